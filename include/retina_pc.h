@@ -1,0 +1,126 @@
+/*
+ * retina_pc.h — C ABI of the MI355X packet-stage filter (drop-in for Retina's packet stage).
+ *
+ * Replaces, per batch of mbufs, what the reference does per mbuf:
+ *   - Subscription::continue_packet            core/src/subscription/mod.rs:125-127
+ *     -> the filtergen-generated packet_continue(mbuf, core_id) -> Actions
+ *        (type PacketContFn, core/src/filter/mod.rs:49; emitted at filtergen/src/lib.rs:336-339)
+ *   - the PacketContinue gate + L4Context::new in Subscription::process_packet
+ *                                              core/src/subscription/mod.rs:94-116,
+ *                                              core/src/conntrack/pdu.rs:86-171
+ *   - packet-level callbacks fired inside packet_continue (ZcFrame / Payload subscriptions,
+ *     filtergen/src/data.rs:299-331), reported as per-packet "statement masks" that name the
+ *     callback sites in generated-code order; the host invokes the callbacks.
+ *   - filtergen itself (filtergen/src/lib.rs:241-385, packet layer): rtn_program_compile turns a
+ *     subscription spec (the #[subscription("spec.toml")] TOML format, filtergen/src/parse.rs)
+ *     into a tree-specialised HIP kernel.
+ * The reference callers are core/src/lcore/rx_core.rs:117-141 (online) and
+ * core/src/runtime/offline.rs:67-82 (pcap). See INTEGRATION.md for the Rust extern "C" binding.
+ *
+ * Conventions: every function returns 0 on success or a negative errno-style code; the message
+ * of the last failure on the calling thread is available from rtn_last_error(). No C++
+ * exceptions cross this boundary. Pointers in rtn_batch_t / rtn_pc_out_t are device pointers
+ * (hipMalloc'd) unless stated. A context is thread-compatible, not thread-safe: use one per
+ * RX thread/stream (like the reference's per-lcore Subscription use).
+ */
+#ifndef RETINA_PC_H
+#define RETINA_PC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RTN_OK 0
+#define RTN_EINVAL (-22)   /* bad argument or layout */
+#define RTN_EFILTER (-74)  /* filter / subscription spec rejected (what filtergen would refuse) */
+#define RTN_EDEVICE (-5)   /* HIP runtime or device failure */
+#define RTN_ECOMPILE (-38) /* kernel compilation (hiprtc) failed */
+#define RTN_ERANGE (-34)   /* output buffer too small */
+
+typedef struct rtn_program rtn_program_t; /* compiled subscription set (host only)        */
+typedef struct rtn_pc rtn_pc_t;           /* program loaded on one device, ready to run  */
+
+/* Compacted L4Context of a forwarded packet (PacketContinue && L4Context::new Ok). 32 bytes. */
+typedef struct rtn_l4ctx {
+  uint32_t pkt_idx;     /* index of the packet within the batch                          */
+  uint32_t src_ip4;     /* u32::from(Ipv4Addr) (host order); 0 for IPv6, see addr6 array  */
+  uint32_t dst_ip4;
+  uint32_t ports;       /* src_port | dst_port << 16                                      */
+  uint32_t seq_no;      /* TCP only (0 for UDP)                                           */
+  uint32_t ack_no;      /* TCP only                                                        */
+  uint32_t off_len;     /* L4Context.offset | L4Context.length << 16                     */
+  uint32_t proto_flags; /* proto (6/17) | tcp flags << 8 | ip version (4/6) << 16          */
+} rtn_l4ctx_t;
+
+/* A batch of frames laid out for coalesced HBM reads: slot i (stride bytes, a multiple of 64)
+ * holds the first min(data_len[i], stride) bytes of frame i. stride >= 128 is always valid;
+ * stride 64 is valid when every data_len <= 64 (else counters[3] bit 0 is raised). */
+typedef struct rtn_batch {
+  const uint8_t* slab;
+  uint64_t stride;
+  const uint16_t* data_len; /* Mbuf::data_len of each frame (mbuf.rs:95-97) */
+  uint32_t n;
+  uint32_t core_id;         /* the calling lcore (passed to CoreId callbacks by the host) */
+} rtn_batch_t;
+
+/* Outputs, segmented per 64-frame group g = i / 64: entry j of group g is at [g * 64 + j];
+ * group g holds popcount(bitmap[g]) entries, in frame order. */
+typedef struct rtn_pc_out {
+  uint64_t* pc_bitmap;   /* [ceil(n/64)]  Actions.data contains PacketContinue               */
+  uint64_t* fwd_bitmap;  /* [ceil(n/64)]  ... and L4Context::new succeeded (goes to conntrack) */
+  rtn_l4ctx_t* l4;       /* [ceil(n/64)*64]                                                   */
+  uint8_t* addr6;        /* optional [ceil(n/64)*64][32]: IPv6 src|dst bytes of IPv6 records  */
+  uint64_t* dlv_bitmap;  /* [ceil(n/64)] frames with >= 1 packet-level callback (if any)     */
+  uint64_t* dlv_records; /* [ceil(n/64)*64][1 + deliver_words]: frame index, statement mask  */
+  uint32_t* counters;    /* optional [4]: pc, fwd, dlv totals, status bits; zeroed per run   */
+} rtn_pc_out_t;
+
+typedef struct rtn_program_info {
+  uint32_t n_subscriptions;
+  uint32_t n_deliver_stmts; /* packet-level callback sites in the generated code              */
+  uint32_t deliver_words;   /* u64 words per statement mask (0 if no packet-level callbacks)  */
+  uint32_t tree_size;       /* nodes of the collapsed PacketContinue tree                     */
+} rtn_program_info_t;
+
+const char* rtn_last_error(void);
+
+/* filtergen: subscription spec (TOML text, [[subscriptions]] filter/datatypes/callback) */
+int32_t rtn_program_compile(const char* spec, size_t len, rtn_program_t** out);
+/* Convenience: a single subscription (filter string + comma-separated datatypes + callback). */
+int32_t rtn_program_compile_filter(const char* filter, const char* datatypes, const char* callback,
+                                   rtn_program_t** out);
+int32_t rtn_program_info(const rtn_program_t* p, rtn_program_info_t* info);
+/* Text outputs: return the length needed (excluding NUL); copy at most cap-1 bytes + NUL. */
+size_t rtn_program_tree(const rtn_program_t* p, char* buf, size_t cap);   /* PTree Display   */
+size_t rtn_program_rust(const rtn_program_t* p, char* buf, size_t cap);   /* filtergen view   */
+size_t rtn_program_source(const rtn_program_t* p, char* buf, size_t cap); /* full HIP source  */
+/* Statement k of a deliver mask -> subscription index / Payload flag. */
+int32_t rtn_program_deliver_table(const rtn_program_t* p, uint32_t* sub_ids, uint8_t* is_payload,
+                                  uint32_t cap);
+/* Compile the program's kernel for gfx950 (hiprtc; needs no GPU). Returns code-object bytes. */
+int32_t rtn_program_code_object(rtn_program_t* p, const uint8_t** data, size_t* len);
+void rtn_program_destroy(rtn_program_t* p);
+
+/* Load a program on `device` (compiles on first use; cached per process). */
+int32_t rtn_pc_create(const char* spec, size_t len, int device, rtn_pc_t** out);
+int32_t rtn_pc_create_from_program(rtn_program_t* p, int device, rtn_pc_t** out);
+/* Launch on `stream` (a hipStream_t, NULL = default). Asynchronous. */
+int32_t rtn_pc_run(rtn_pc_t* pc, const rtn_batch_t* in, rtn_pc_out_t* out, void* stream);
+/* Workgroups per launch (0 = default). */
+int32_t rtn_pc_set_grid(rtn_pc_t* pc, uint32_t blocks);
+int32_t rtn_pc_destroy(rtn_pc_t* pc);
+
+/* Bytes the caller must allocate for each output array for n frames (for deliver_words). */
+size_t rtn_out_bitmap_bytes(uint32_t n);
+size_t rtn_out_l4_bytes(uint32_t n);
+size_t rtn_out_addr6_bytes(uint32_t n);
+size_t rtn_out_dlv_bytes(uint32_t n, uint32_t deliver_words);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RETINA_PC_H */

@@ -1,0 +1,104 @@
+"""Build the native parts in-tree (no setuptools, no JIT cache): the filter compiler + HIP runtime
+shared library, the rtnc CLI, and an ahead-of-time gfx950 compile of the kernel template as a
+build check. Outputs land in retina_amd/_lib/ (git-ignored, shipped to the GPU box by gpurun)."""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+ROOT = PKG.parent
+CSRC = PKG / "csrc"
+LIB = PKG / "_lib"
+ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
+ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0]
+
+FILTERGEN_SRCS = ["ast.cpp", "parser.cpp", "filter.cpp", "ptree.cpp", "codegen.cpp"]
+SO_NAME = "libretina_pc.so"
+
+
+def _run(cmd: list[str], cwd: Path | None = None) -> None:
+    r = subprocess.run(cmd, cwd=cwd, capture_output=True, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(" ".join(cmd) + "\n" + r.stdout + r.stderr)
+        raise RuntimeError(f"build step failed: {cmd[0]} (exit {r.returncode})")
+
+
+def _stale(target: Path, deps: list[Path]) -> bool:
+    if not target.exists():
+        return True
+    t = target.stat().st_mtime
+    return any(d.stat().st_mtime > t for d in deps)
+
+
+def _gen_kernel_inc() -> Path:
+    src = CSRC / "kernels" / "pc_kernel.hip"
+    inc = CSRC / "runtime" / "pc_kernel_src.inc"
+    text = src.read_text()
+    delim = "RTNSRC"
+    assert f"){delim}\"" not in text
+    body = f'static const char* const kPcKernelSrc = R"{delim}(' + text + f'){delim}";\n'
+    if not inc.exists() or inc.read_text() != body:
+        inc.write_text(body)
+    return inc
+
+
+def build_library(force: bool = False) -> Path:
+    LIB.mkdir(exist_ok=True)
+    inc = _gen_kernel_inc()
+    fg = [CSRC / "filtergen" / s for s in FILTERGEN_SRCS]
+    rt = CSRC / "runtime" / "rtn_runtime.cpp"
+    hdrs = list((CSRC / "filtergen").glob("*.hpp")) + [ROOT / "include" / "retina_pc.h", inc]
+    so = LIB / SO_NAME
+    if force or _stale(so, fg + [rt] + hdrs):
+        cmd = [
+            "g++", "-std=c++17", "-O2", "-fPIC", "-shared", "-Wall", "-Wextra", "-Wno-unused-parameter",
+            "-D__HIP_PLATFORM_AMD__", f"-I{ROOT / 'include'}", f"-I{ROCM / 'include'}",
+            *map(str, fg), str(rt), "-o", str(so),
+            f"-L{ROCM / 'lib'}", f"-Wl,-rpath,{ROCM / 'lib'}", "-lamdhip64", "-lhiprtc",
+        ]
+        _run(cmd)
+    cli = LIB / "rtnc"
+    main = CSRC / "filtergen" / "rtnc_main.cpp"
+    if force or _stale(cli, fg + [main] + hdrs):
+        _run(["g++", "-std=c++17", "-O2", "-Wall", *map(str, fg), str(main), "-o", str(cli)])
+    return so
+
+
+def build_kernel_check() -> Path:
+    """Ahead-of-time hipcc compile of the kernel template with the config-2 filter spliced in
+    (the same translation unit hiprtc builds at run time) to catch template breakage at build."""
+    so = LIB / SO_NAME
+    out = LIB / "pc_kernel_cfg2.hsaco"
+    src = LIB / "pc_kernel_cfg2.hip"
+    tpl = CSRC / "kernels" / "pc_kernel.hip"
+    if not _stale(out, [tpl, so]):
+        return out
+    sys.path.insert(0, str(ROOT))
+    from retina_amd import pc  # noqa: E402
+
+    prog = pc.Program.from_filter("tcp.dst_port = 80", ["ConnRecord"])
+    src.write_text(prog.source)
+    _run([str(ROCM / "bin" / "hipcc"), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "--genco",
+          str(src), "-o", str(out)])
+    return out
+
+
+def build_oracle() -> None:
+    sys.path.insert(0, str(ROOT))
+    from oracle import build as obuild  # noqa: E402
+
+    obuild.build_all()
+
+
+def build_all(force: bool = False) -> None:
+    build_library(force)
+    build_kernel_check()
+    build_oracle()
+
+
+if __name__ == "__main__":
+    build_all(force="--force" in sys.argv)
+    print("built", LIB)

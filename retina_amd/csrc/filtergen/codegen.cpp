@@ -1,0 +1,302 @@
+// PacketContinue code generation (see codegen.hpp for the reference map).
+#include "codegen.hpp"
+
+#include <cstdio>
+#include <map>
+
+namespace rtn {
+namespace {
+
+enum class FT { U8, U16, U32, BOOL, V4, V6 };
+
+struct FieldDef {
+  FT type;
+  const char* hip;  // HIP expression over `v` (rtn_view) producing the accessor's value
+};
+
+// Public accessors of the packet parsers (core/src/protocols/packet/{ipv4,ipv6,tcp,udp}.rs) with
+// their Rust return types. `rtn_l3_*` / `rtn_l4_*` read the fixed header views the kernel builds.
+const std::map<std::string, FieldDef>& fields(const std::string& proto) {
+  static const std::map<std::string, FieldDef> ipv4 = {
+      {"version", {FT::U8, "((rtn_l3_b(v, 0) & 0xf0u) >> 4)"}},              // ipv4.rs:38-40
+      {"ihl", {FT::U8, "(rtn_l3_b(v, 0) & 0x0fu)"}},                          // :44-46
+      {"version_ihl", {FT::U8, "rtn_l3_b(v, 0)"}},                           // :50-52
+      {"dscp", {FT::U8, "(rtn_l3_b(v, 1) >> 2)"}},                            // :56-58
+      {"ecn", {FT::U8, "(rtn_l3_b(v, 1) & 0x03u)"}},                          // :62-64
+      {"dscp_ecn", {FT::U8, "rtn_l3_b(v, 1)"}},                              // :68-70
+      {"type_of_service", {FT::U8, "rtn_l3_b(v, 1)"}},                       // :74-76
+      {"total_length", {FT::U16, "rtn_l3_be16(v, 2)"}},                      // :80-82
+      {"identification", {FT::U16, "rtn_l3_be16(v, 4)"}},                    // :86-88
+      {"flags_to_fragment_offset", {FT::U16, "rtn_l3_be16(v, 6)"}},          // :92-94
+      {"flags", {FT::U8, "(rtn_l3_be16(v, 6) >> 13)"}},                       // :98-100
+      {"rf", {FT::BOOL, "((rtn_l3_be16(v, 6) & 0x8000u) != 0u ? 1u : 0u)"}},  // :104-106
+      {"df", {FT::BOOL, "((rtn_l3_be16(v, 6) & 0x4000u) != 0u ? 1u : 0u)"}},  // :110-112
+      {"mf", {FT::BOOL, "((rtn_l3_be16(v, 6) & 0x2000u) != 0u ? 1u : 0u)"}},  // :116-118
+      {"fragment_offset", {FT::U16, "(rtn_l3_be16(v, 6) & 0x1fffu)"}},        // :122-124
+      {"time_to_live", {FT::U8, "rtn_l3_b(v, 8)"}},                          // :128-130
+      {"protocol", {FT::U8, "rtn_l3_b(v, 9)"}},                              // :134-136
+      {"header_checksum", {FT::U16, "rtn_l3_be16(v, 10)"}},                  // :140-142
+      {"src_addr", {FT::V4, "rtn_l3_be32(v, 12)"}},                          // :146-148
+      {"dst_addr", {FT::V4, "rtn_l3_be32(v, 16)"}},                          // :152-154
+  };
+  static const std::map<std::string, FieldDef> ipv6 = {
+      {"version", {FT::U8, "((rtn_l3_be32(v, 0) & 0xf0000000u) >> 28)"}},    // ipv6.rs:31-34
+      {"dscp", {FT::U8, "((rtn_l3_be32(v, 0) & 0x0fc00000u) >> 22)"}},       // :38-41
+      {"ecn", {FT::U8, "((rtn_l3_be32(v, 0) & 0x00300000u) >> 20)"}},        // :45-48
+      {"traffic_class", {FT::U8, "((rtn_l3_be32(v, 0) & 0x0ff00000u) >> 20)"}},  // :52-55
+      {"flow_label", {FT::U32, "(rtn_l3_be32(v, 0) & 0x000fffffu)"}},         // :59-61
+      {"version_to_flow_label", {FT::U32, "rtn_l3_be32(v, 0)"}},             // :65-67
+      {"payload_length", {FT::U16, "rtn_l3_be16(v, 4)"}},                    // :71-73
+      {"next_header", {FT::U8, "rtn_l3_b(v, 6)"}},                           // :77-79
+      {"hop_limit", {FT::U8, "rtn_l3_b(v, 7)"}},                             // :83-85
+      {"src_addr", {FT::V6, "8"}},                                            // :89-91 (byte offset)
+      {"dst_addr", {FT::V6, "24"}},                                           // :95-97
+  };
+  static const std::map<std::string, FieldDef> tcp = {
+      {"src_port", {FT::U16, "rtn_l4_be16(v, 0)"}},                          // tcp.rs:38-40
+      {"dst_port", {FT::U16, "rtn_l4_be16(v, 2)"}},                          // :44-46
+      {"seq_no", {FT::U32, "rtn_l4_be32(v, 4)"}},                            // :50-52
+      {"ack_no", {FT::U32, "rtn_l4_be32(v, 8)"}},                            // :56-58
+      {"data_offset", {FT::U8, "((rtn_l4_b(v, 12) & 0xf0u) >> 4)"}},          // :62-64
+      {"reserved", {FT::U8, "(rtn_l4_b(v, 12) & 0x0fu)"}},                    // :68-70
+      {"data_offset_to_ns", {FT::U8, "rtn_l4_b(v, 12)"}},                    // :74-76
+      {"flags", {FT::U8, "rtn_l4_b(v, 13)"}},                                // :80-82
+      {"window", {FT::U16, "rtn_l4_be16(v, 14)"}},                           // :86-88
+      {"checksum", {FT::U16, "rtn_l4_be16(v, 16)"}},                         // :92-94
+      {"urgent_pointer", {FT::U16, "rtn_l4_be16(v, 18)"}},                   // :98-100
+      {"ns", {FT::U8, "(rtn_l4_b(v, 12) & 0x01u)"}},                          // :106-108
+      {"cwr", {FT::U8, "((rtn_l4_b(v, 13) >> 7) & 1u)"}},                     // :112-114
+      {"ece", {FT::U8, "((rtn_l4_b(v, 13) >> 6) & 1u)"}},                     // :118-120
+      {"urg", {FT::U8, "((rtn_l4_b(v, 13) >> 5) & 1u)"}},                     // :124-126
+      {"ack", {FT::U8, "((rtn_l4_b(v, 13) >> 4) & 1u)"}},                     // :130-132
+      {"psh", {FT::U8, "((rtn_l4_b(v, 13) >> 3) & 1u)"}},                     // :136-138
+      {"rst", {FT::U8, "((rtn_l4_b(v, 13) >> 2) & 1u)"}},                     // :142-144
+      {"syn", {FT::U8, "((rtn_l4_b(v, 13) >> 1) & 1u)"}},                     // :148-150
+      {"fin", {FT::U8, "(rtn_l4_b(v, 13) & 1u)"}},                            // :154-156
+      {"synack", {FT::U8, "((rtn_l4_b(v, 13) & 0x12u) != 0u ? 1u : 0u)"}},    // :160-162 (SYN or ACK)
+  };
+  static const std::map<std::string, FieldDef> udp = {
+      {"src_port", {FT::U16, "rtn_l4_be16(v, 0)"}},                          // udp.rs:24-26
+      {"dst_port", {FT::U16, "rtn_l4_be16(v, 2)"}},                          // :30-32
+      {"length", {FT::U16, "rtn_l4_be16(v, 4)"}},                            // :36-38
+      {"checksum", {FT::U16, "rtn_l4_be16(v, 6)"}},                          // :42-44
+  };
+  static const std::map<std::string, FieldDef> none;
+  if (proto == "ipv4") return ipv4;
+  if (proto == "ipv6") return ipv6;
+  if (proto == "tcp") return tcp;
+  if (proto == "udp") return udp;
+  return none;
+}
+
+const char* camel(const std::string& p) {
+  if (p == "ethernet") return "Ethernet";
+  if (p == "ipv4") return "Ipv4";
+  if (p == "ipv6") return "Ipv6";
+  if (p == "tcp") return "Tcp";
+  if (p == "udp") return "Udp";
+  return "?";
+}
+
+uint64_t type_max(FT t) {
+  switch (t) {
+    case FT::U8: return 0xff;
+    case FT::U16: return 0xffff;
+    case FT::U32: return 0xffffffffull;
+    default: return 0;
+  }
+}
+
+bool is_int(FT t) { return t == FT::U8 || t == FT::U16 || t == FT::U32; }
+
+std::string u32lit(uint64_t v) { return std::to_string(v) + "u"; }
+
+struct Gen {
+  PacketProgram& prog;
+  std::string hip, rust;
+
+  [[noreturn]] void type_error(const Predicate& p, const std::string& why) {
+    throw FilterError("filter does not type-check (" + p.str() + "): " + why);
+  }
+
+  // binary_to_tokens (utils.rs:18-249): returns {hip_expr, rust_expr}
+  std::pair<std::string, std::string> binary(const Predicate& p) {
+    const auto& tab = fields(p.protocol);
+    auto it = tab.find(p.field);
+    if (it == tab.end()) type_error(p, "no method named `" + p.field + "` on `" + camel(p.protocol) + "`");
+    const FieldDef& fd = it->second;
+    const std::string racc = p.protocol + "." + p.field + "()";
+    const Value& val = p.value;
+    auto bad_op = [&]() { type_error(p, std::string("Invalid binary operation `") + binop_str(p.op) + "` for value"); };
+    switch (val.kind) {
+      case VKind::Int: {
+        const char* op = nullptr;
+        switch (p.op) {
+          case BinOp::Eq: op = "=="; break;
+          case BinOp::Ne: op = "!="; break;
+          case BinOp::Ge: op = ">="; break;
+          case BinOp::Le: op = "<="; break;
+          case BinOp::Gt: op = ">"; break;
+          case BinOp::Lt: op = "<"; break;
+          default: bad_op();
+        }
+        if (!is_int(fd.type)) type_error(p, "mismatched types: integer literal against a non-integer accessor");
+        if (val.i > type_max(fd.type)) type_error(p, "literal out of range for the accessor's type");
+        return {"(" + std::string(fd.hip) + " " + op + " " + u32lit(val.i) + ")",
+                racc + " " + op + " " + std::to_string(val.i)};
+      }
+      case VKind::IntRange: {
+        if (p.op != BinOp::In) bad_op();
+        if (!is_int(fd.type)) type_error(p, "mismatched types: integer literal against a non-integer accessor");
+        if (val.to > type_max(fd.type) || val.i > type_max(fd.type))
+          type_error(p, "literal out of range for the accessor's type");
+        return {"((" + std::string(fd.hip) + " >= " + u32lit(val.i) + ") && (" + fd.hip + " <= " + u32lit(val.to) + "))",
+                racc + " >= " + std::to_string(val.i) + " && " + racc + " <= " + std::to_string(val.to)};
+      }
+      case VKind::Ipv4: {
+        if (p.op != BinOp::Eq && p.op != BinOp::Ne && p.op != BinOp::In) bad_op();
+        if (fd.type == FT::V6) type_error(p, "the trait `From<Ipv6Addr>` is not implemented for `u32`");
+        uint32_t addr = val.v4.addr, mask = val.v4.netmask(), net = addr & mask;
+        bool ne = p.op == BinOp::Ne;
+        std::string x = fd.hip;
+        std::string rx = "u32::from(" + racc + ")";
+        if (val.v4.prefix == 32)
+          return {"(" + x + (ne ? " != " : " == ") + u32lit(addr) + ")",
+                  rx + (ne ? " != " : " == ") + std::to_string(addr)};
+        return {"((" + x + " & " + u32lit(mask) + ")" + (ne ? " != " : " == ") + u32lit(net) + ")",
+                rx + " & " + std::to_string(mask) + (ne ? " != " : " == ") + std::to_string(net)};
+      }
+      case VKind::Ipv6: {
+        if (p.op != BinOp::Eq && p.op != BinOp::Ne && p.op != BinOp::In) bad_op();
+        if (fd.type == FT::V4) type_error(p, "the trait `From<Ipv4Addr>` is not implemented for `u128`");
+        U128 addr = val.v6.addr, mask = val.v6.netmask(), net = addr & mask;
+        bool full = val.v6.prefix == 128;
+        bool ne = p.op == BinOp::Ne;
+        uint32_t aw[4] = {(uint32_t)(addr.hi >> 32), (uint32_t)addr.hi, (uint32_t)(addr.lo >> 32), (uint32_t)addr.lo};
+        uint32_t mw[4] = {(uint32_t)(mask.hi >> 32), (uint32_t)mask.hi, (uint32_t)(mask.lo >> 32), (uint32_t)mask.lo};
+        uint32_t nw[4] = {(uint32_t)(net.hi >> 32), (uint32_t)net.hi, (uint32_t)(net.lo >> 32), (uint32_t)net.lo};
+        std::string conj;
+        for (int k = 0; k < 4; ++k) {
+          std::string word;
+          if (fd.type == FT::V6) word = "rtn_l3_be32(v, " + std::string(fd.hip) + " + " + std::to_string(4 * k) + ")";
+          else word = k == 3 ? std::string(fd.hip) : std::string("0u");
+          std::string term = full ? "(" + word + " == " + u32lit(aw[k]) + ")"
+                                  : "((" + word + " & " + u32lit(mw[k]) + ") == " + u32lit(nw[k]) + ")";
+          conj += (k ? " && " : "") + term;
+        }
+        std::string rx = "u128::from(" + racc + ")";
+        std::string hexpr = ne ? "(!(" + conj + "))" : "(" + conj + ")";
+        if (full) return {hexpr, rx + (ne ? " != " : " == ") + addr.to_dec()};
+        return {hexpr, rx + " & " + mask.to_dec() + (ne ? " != " : " == ") + net.to_dec()};
+      }
+      case VKind::Text:
+        type_error(p, "string values cannot be compared with packet header accessors");
+      case VKind::Byte:
+        type_error(p, "byte values cannot be compared with packet header accessors");
+    }
+    type_error(p, "unsupported value");
+  }
+
+  static std::string ind(int d) { return std::string(2 * d, ' '); }
+
+  // update_body (utils.rs:251-285) at the PacketContinue layer
+  void update_body(const PNode& n, int d) {
+    if (!n.actions.drop()) {
+      hip += ind(d) + "act |= " + u32lit(n.actions.data) + ";\n";
+      rust += ind(d) + "result.push(Actions{data:" + std::to_string(n.actions.data) + ",terminal:" +
+              std::to_string(n.actions.terminal) + "});\n";
+    }
+    for (auto& dv : n.deliver) {
+      const SubscriptionSpec& spec = prog.subs.at(dv.id);
+      if (spec.level != Level::Packet) throw FilterError("internal: non-packet delivery at PacketContinue");
+      // build_packet_callback (data.rs:299-331) / build_packet_params (data.rs:262-297)
+      std::string ty, params;
+      for (auto& dt : spec.datatypes) {
+        if (!params.empty()) params += ", ";
+        if (dt.level == Level::Packet) {
+          ty = dt.as_str;
+          params += "p";
+        } else if (dt.as_str == "FilterStr") {
+          params += "&\"" + spec.filter + "\"";
+        } else if (dt.as_str == "CoreId") {
+          params += "core_id";
+        } else {
+          throw FilterError("Invalid datatype in packet callback: " + dt.as_str);
+        }
+      }
+      if (ty != "ZcFrame" && ty != "Payload") throw FilterError("unsupported packet datatype " + ty);
+      uint32_t k = (uint32_t)prog.delivers.size();
+      prog.delivers.push_back(DeliverStmt{(uint32_t)dv.id, ty == "Payload", spec.callback});
+      std::string bit = "dm[" + std::to_string(k / 64) + "] |= (1ull << " + std::to_string(k % 64) + ");";
+      if (ty == "Payload") hip += ind(d) + "if (v.payload_ok) { " + bit + " }\n";
+      else hip += ind(d) + bit + "\n";
+      rust += ind(d) + "if let Some(p) = " + ty + "::from_mbuf(mbuf) { " + spec.callback + "(" + params + "); }\n";
+    }
+  }
+
+  // gen_packet_filter_util (packet_filter.rs:31-73)
+  void children(const PNode& n, int d) {
+    bool first_unary = true;
+    for (auto& c : n.children) {
+      if (!c.pred.on_packet()) continue;
+      if (c.pred.is_unary()) {
+        const std::string& proto = c.pred.protocol;
+        std::string cond;
+        if (proto == "ipv4") cond = "v.v4";
+        else if (proto == "ipv6") cond = "v.v6";
+        else if (proto == "tcp") cond = "v.tcp";
+        else if (proto == "udp") cond = "v.udp";
+        else throw FilterError("internal: unexpected packet protocol " + proto);
+        hip += ind(d) + (first_unary ? "if (" : "else if (") + cond + ") {\n";
+        rust += ind(d) + (first_unary ? "if let Ok(" : "else if let Ok(") + proto + ") = parse_to::<" + camel(proto) +
+                ">(" + n.pred.protocol + ") {\n";
+        first_unary = false;
+      } else {
+        auto ex = binary(c.pred);
+        hip += ind(d) + (c.if_else ? "else if " : "if ") + ex.first + " {\n";
+        rust += ind(d) + (c.if_else ? "else if " : "if ") + ex.second + " {\n";
+      }
+      children(c, d + 1);
+      update_body(c, d + 1);
+      hip += ind(d) + "}\n";
+      rust += ind(d) + "}\n";
+    }
+  }
+};
+
+}  // namespace
+
+PacketProgram compile_packet_program(const std::vector<SubscriptionSpec>& subs) {
+  PacketProgram prog;
+  prog.subs = subs;
+  for (auto& s : prog.subs) s.validate_spec();
+  prog.tree = filter_subtree(FilterLayer::PacketContinue, prog.subs);
+  const PNode& root = prog.tree.root;
+  if (root.actions.terminal != 0) throw FilterError("internal: terminal actions at PacketContinue");
+
+  Gen g{prog, "", ""};
+  // gen_packet_filter (packet_filter.rs:7-29) + add_root_pred (utils.rs:363-379)
+  bool any_pkt_child = false;
+  for (auto& c : root.children) any_pkt_child = any_pkt_child || c.pred.on_packet();
+  bool root_body = !root.actions.drop() || !root.deliver.empty();
+  bool body_nonempty = root_body || any_pkt_child;
+  prog.wraps_ethernet = body_nonempty && any_pkt_child;
+  int d = prog.wraps_ethernet ? 2 : 1;
+  if (prog.wraps_ethernet) {
+    g.hip += "  if (v.eth_ok) {\n";
+    g.rust += "  if let Ok(ethernet) = parse_to::<Ethernet>(mbuf) {\n";
+  }
+  if (root_body) g.update_body(root, d);
+  g.children(root, d);
+  if (prog.wraps_ethernet) {
+    g.hip += "  }\n";
+    g.rust += "  }\n";
+  }
+  prog.hip_body = "__device__ __forceinline__ void rtn_filter(const rtn_view& v, rtn_u32& act, rtn_u64* dm) {\n"
+                  "  (void)v; (void)dm;\n" +
+                  g.hip + "}\n";
+  prog.rust_listing = "let mut result = Actions::new();\n" + g.rust + "result\n";
+  return prog;
+}
+
+}  // namespace rtn

@@ -1,0 +1,318 @@
+// C-ABI runtime: compile subscription specs, build the specialised gfx950 kernel with hiprtc,
+// load it and launch it. See include/retina_pc.h for the contract and reference map.
+#include "retina_pc.h"
+
+#include <hip/hip_runtime.h>
+#include <hip/hiprtc.h>
+
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../filtergen/codegen.hpp"
+
+namespace {
+
+#include "pc_kernel_src.inc"  // kPcKernelSrc: csrc/kernels/pc_kernel.hip as a string literal
+
+thread_local std::string g_err;
+
+int32_t fail(int32_t code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+size_t copy_text(const std::string& s, char* buf, size_t cap) {
+  if (buf && cap > 0) {
+    size_t n = s.size() < cap - 1 ? s.size() : cap - 1;
+    memcpy(buf, s.data(), n);
+    buf[n] = 0;
+  }
+  return s.size();
+}
+
+std::string build_source(const rtn::PacketProgram& prog) {
+  const std::string tpl = kPcKernelSrc;
+  const std::string marker = "//@@RTN_FILTER@@";
+  size_t at = tpl.find(marker);
+  std::string head = "#define RTN_DELIVER_WORDS " + std::to_string(prog.deliver_words()) + "\n";
+  return head + tpl.substr(0, at) + prog.hip_body + tpl.substr(at + marker.size());
+}
+
+uint64_t fnv1a(const std::string& s) {
+  uint64_t h = 1469598103934665603ull;
+  for (unsigned char c : s) h = (h ^ c) * 1099511628211ull;
+  return h;
+}
+
+std::mutex g_cache_mu;
+std::map<uint64_t, std::shared_ptr<std::vector<uint8_t>>> g_cache;  // source hash -> code object
+
+int32_t compile_code_object(const std::string& src, std::shared_ptr<std::vector<uint8_t>>& out) {
+  const uint64_t h = fnv1a(src);
+  {
+    std::lock_guard<std::mutex> lk(g_cache_mu);
+    auto it = g_cache.find(h);
+    if (it != g_cache.end()) {
+      out = it->second;
+      return RTN_OK;
+    }
+  }
+  hiprtcProgram prog;
+  if (hiprtcCreateProgram(&prog, src.c_str(), "rtn_pc_kernel.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS)
+    return fail(RTN_ECOMPILE, "hiprtcCreateProgram failed");
+  std::string arch = "--offload-arch=gfx950";
+  if (const char* a = getenv("RTN_OFFLOAD_ARCH")) arch = std::string("--offload-arch=") + a;
+  const char* opts[] = {arch.c_str(), "-O3", "-std=c++17"};
+  hiprtcResult r = hiprtcCompileProgram(prog, 3, opts);
+  size_t ls = 0;
+  hiprtcGetProgramLogSize(prog, &ls);
+  std::string log(ls, '\0');
+  if (ls) hiprtcGetProgramLog(prog, &log[0]);
+  if (r != HIPRTC_SUCCESS) {
+    hiprtcDestroyProgram(&prog);
+    return fail(RTN_ECOMPILE, std::string("hiprtc: ") + hiprtcGetErrorString(r) + "\n" + log);
+  }
+  size_t cs = 0;
+  hiprtcGetCodeSize(prog, &cs);
+  auto code = std::make_shared<std::vector<uint8_t>>(cs);
+  hiprtcGetCode(prog, reinterpret_cast<char*>(code->data()));
+  hiprtcDestroyProgram(&prog);
+  {
+    std::lock_guard<std::mutex> lk(g_cache_mu);
+    g_cache[h] = code;
+  }
+  out = code;
+  return RTN_OK;
+}
+
+// kernel argument block; must match struct rtn_args in pc_kernel.hip
+struct KArgs {
+  const unsigned char* slab;
+  uint64_t stride;
+  const unsigned short* dlen;
+  uint32_t n;
+  uint32_t flags;
+  uint64_t* pc_bm;
+  uint64_t* fwd_bm;
+  rtn_l4ctx_t* recs;
+  unsigned char* addr6;
+  uint64_t* dlv_bm;
+  uint64_t* dlv_recs;
+  uint32_t* counters;
+};
+
+}  // namespace
+
+struct rtn_program {
+  rtn::PacketProgram prog;
+  std::string source;
+  std::shared_ptr<std::vector<uint8_t>> code;
+};
+
+struct rtn_pc {
+  rtn_program* owned = nullptr;  // set when created from a spec
+  const rtn_program* program = nullptr;
+  int device = 0;
+  hipModule_t module = nullptr;
+  hipFunction_t fn = nullptr;
+  uint32_t blocks = 0;
+  uint32_t* scratch_counters = nullptr;  // used when the caller passes no counters
+};
+
+extern "C" {
+
+const char* rtn_last_error(void) { return g_err.c_str(); }
+
+int32_t rtn_program_compile(const char* spec, size_t len, rtn_program_t** out) {
+  if (!spec || !out) return fail(RTN_EINVAL, "null argument");
+  try {
+    auto subs = rtn::parse_subscription_toml(std::string(spec, len));
+    auto p = std::make_unique<rtn_program>();
+    p->prog = rtn::compile_packet_program(subs);
+    p->source = build_source(p->prog);
+    *out = p.release();
+    return RTN_OK;
+  } catch (const rtn::FilterError& e) {
+    return fail(RTN_EFILTER, e.what());
+  } catch (const std::exception& e) {
+    return fail(RTN_EFILTER, std::string("internal error: ") + e.what());
+  }
+}
+
+int32_t rtn_program_compile_filter(const char* filter, const char* datatypes, const char* callback,
+                                   rtn_program_t** out) {
+  if (!filter || !datatypes || !out) return fail(RTN_EINVAL, "null argument");
+  try {
+    rtn::SubscriptionSpec s(filter, callback ? callback : "cb");
+    std::string dts = datatypes, tok;
+    auto flush = [&]() {
+      size_t b = tok.find_first_not_of(" \t"), e = tok.find_last_not_of(" \t");
+      if (b != std::string::npos) {
+        std::string t = tok.substr(b, e - b + 1);
+        rtn::DataType dt;
+        if (!rtn::lookup_datatype(t, dt)) throw rtn::FilterError("Invalid datatype: " + t);
+        s.add_datatype(dt);
+      }
+      tok.clear();
+    };
+    for (char c : dts) {
+      if (c == ',') flush();
+      else tok.push_back(c);
+    }
+    flush();
+    if (s.datatypes.empty()) throw rtn::FilterError("subscription without datatypes");
+    auto p = std::make_unique<rtn_program>();
+    p->prog = rtn::compile_packet_program({s});
+    p->source = build_source(p->prog);
+    *out = p.release();
+    return RTN_OK;
+  } catch (const rtn::FilterError& e) {
+    return fail(RTN_EFILTER, e.what());
+  } catch (const std::exception& e) {
+    return fail(RTN_EFILTER, std::string("internal error: ") + e.what());
+  }
+}
+
+int32_t rtn_program_info(const rtn_program_t* p, rtn_program_info_t* info) {
+  if (!p || !info) return fail(RTN_EINVAL, "null argument");
+  info->n_subscriptions = (uint32_t)p->prog.subs.size();
+  info->n_deliver_stmts = (uint32_t)p->prog.delivers.size();
+  info->deliver_words = p->prog.deliver_words();
+  info->tree_size = (uint32_t)p->prog.tree.size;
+  return RTN_OK;
+}
+
+size_t rtn_program_tree(const rtn_program_t* p, char* buf, size_t cap) {
+  return p ? copy_text(p->prog.tree.pprint(), buf, cap) : 0;
+}
+size_t rtn_program_rust(const rtn_program_t* p, char* buf, size_t cap) {
+  return p ? copy_text(p->prog.rust_listing, buf, cap) : 0;
+}
+size_t rtn_program_source(const rtn_program_t* p, char* buf, size_t cap) {
+  return p ? copy_text(p->source, buf, cap) : 0;
+}
+
+int32_t rtn_program_deliver_table(const rtn_program_t* p, uint32_t* sub_ids, uint8_t* is_payload, uint32_t cap) {
+  if (!p) return fail(RTN_EINVAL, "null program");
+  const auto& d = p->prog.delivers;
+  if (cap < d.size()) return fail(RTN_ERANGE, "deliver table capacity too small");
+  for (size_t k = 0; k < d.size(); ++k) {
+    if (sub_ids) sub_ids[k] = d[k].sub_id;
+    if (is_payload) is_payload[k] = d[k].payload ? 1 : 0;
+  }
+  return RTN_OK;
+}
+
+int32_t rtn_program_code_object(rtn_program_t* p, const uint8_t** data, size_t* len) {
+  if (!p || !data || !len) return fail(RTN_EINVAL, "null argument");
+  if (!p->code) {
+    int32_t rc = compile_code_object(p->source, p->code);
+    if (rc) return rc;
+  }
+  *data = p->code->data();
+  *len = p->code->size();
+  return RTN_OK;
+}
+
+void rtn_program_destroy(rtn_program_t* p) { delete p; }
+
+int32_t rtn_pc_create_from_program(rtn_program_t* p, int device, rtn_pc_t** out) {
+  if (!p || !out) return fail(RTN_EINVAL, "null argument");
+  const uint8_t* code;
+  size_t len;
+  int32_t rc = rtn_program_code_object(p, &code, &len);
+  if (rc) return rc;
+  auto pc = std::make_unique<rtn_pc>();
+  pc->program = p;
+  pc->device = device;
+  if (hipSetDevice(device) != hipSuccess) return fail(RTN_EDEVICE, "hipSetDevice failed");
+  hipError_t e = hipModuleLoadData(&pc->module, code);
+  if (e != hipSuccess) return fail(RTN_EDEVICE, std::string("hipModuleLoadData: ") + hipGetErrorString(e));
+  e = hipModuleGetFunction(&pc->fn, pc->module, "rtn_pc_kernel");
+  if (e != hipSuccess) return fail(RTN_EDEVICE, std::string("hipModuleGetFunction: ") + hipGetErrorString(e));
+  e = hipMalloc(&pc->scratch_counters, 16);
+  if (e != hipSuccess) return fail(RTN_EDEVICE, std::string("hipMalloc: ") + hipGetErrorString(e));
+  if (const char* g = getenv("RTN_GRID")) pc->blocks = (uint32_t)strtoul(g, nullptr, 10);
+  *out = pc.release();
+  return RTN_OK;
+}
+
+int32_t rtn_pc_create(const char* spec, size_t len, int device, rtn_pc_t** out) {
+  rtn_program_t* p = nullptr;
+  int32_t rc = rtn_program_compile(spec, len, &p);
+  if (rc) return rc;
+  rc = rtn_pc_create_from_program(p, device, out);
+  if (rc) {
+    rtn_program_destroy(p);
+    return rc;
+  }
+  (*out)->owned = p;
+  return RTN_OK;
+}
+
+int32_t rtn_pc_set_grid(rtn_pc_t* pc, uint32_t blocks) {
+  if (!pc) return fail(RTN_EINVAL, "null context");
+  pc->blocks = blocks;
+  return RTN_OK;
+}
+
+int32_t rtn_pc_run(rtn_pc_t* pc, const rtn_batch_t* in, rtn_pc_out_t* out, void* stream) {
+  if (!pc || !in || !out) return fail(RTN_EINVAL, "null argument");
+  if (in->n == 0) return RTN_OK;
+  if (!in->slab || !in->data_len) return fail(RTN_EINVAL, "batch slab/data_len missing");
+  if (in->stride < 64 || in->stride % 64 != 0) return fail(RTN_EINVAL, "stride must be a positive multiple of 64");
+  if ((reinterpret_cast<uintptr_t>(in->slab) & 15u) != 0) return fail(RTN_EINVAL, "slab must be 16-byte aligned");
+  if (!out->pc_bitmap || !out->fwd_bitmap || !out->l4) return fail(RTN_EINVAL, "pc_bitmap/fwd_bitmap/l4 required");
+  const uint32_t dw = pc->program->prog.deliver_words();
+  if (dw > 0 && (!out->dlv_bitmap || !out->dlv_records))
+    return fail(RTN_EINVAL, "program has packet-level callbacks: dlv_bitmap/dlv_records required");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  uint32_t* counters = out->counters ? out->counters : pc->scratch_counters;
+  hipError_t e = hipMemsetAsync(counters, 0, 16, s);
+  if (e != hipSuccess) return fail(RTN_EDEVICE, std::string("hipMemsetAsync: ") + hipGetErrorString(e));
+  KArgs a;
+  a.slab = in->slab;
+  a.stride = in->stride;
+  a.dlen = in->data_len;
+  a.n = in->n;
+  a.flags = out->addr6 ? 1u : 0u;
+  a.pc_bm = out->pc_bitmap;
+  a.fwd_bm = out->fwd_bitmap;
+  a.recs = out->l4;
+  a.addr6 = out->addr6;
+  a.dlv_bm = out->dlv_bitmap;
+  a.dlv_recs = out->dlv_records;
+  a.counters = counters;
+  const uint32_t groups = (in->n + 63u) / 64u;
+  uint32_t blocks = pc->blocks ? pc->blocks : 2048u;
+  const uint32_t need = (groups + 3u) / 4u;
+  if (blocks > need) blocks = need;
+  if (blocks == 0) blocks = 1;
+  void* params[] = {&a};
+  e = hipModuleLaunchKernel(pc->fn, blocks, 1, 1, 256, 1, 1, 0, s, params, nullptr);
+  if (e != hipSuccess) return fail(RTN_EDEVICE, std::string("hipModuleLaunchKernel: ") + hipGetErrorString(e));
+  return RTN_OK;
+}
+
+int32_t rtn_pc_destroy(rtn_pc_t* pc) {
+  if (!pc) return RTN_OK;
+  if (pc->scratch_counters) (void)hipFree(pc->scratch_counters);
+  if (pc->module) (void)hipModuleUnload(pc->module);
+  if (pc->owned) rtn_program_destroy(pc->owned);
+  delete pc;
+  return RTN_OK;
+}
+
+size_t rtn_out_bitmap_bytes(uint32_t n) { return (size_t)((n + 63u) / 64u) * 8u; }
+size_t rtn_out_l4_bytes(uint32_t n) { return (size_t)((n + 63u) / 64u) * 64u * sizeof(rtn_l4ctx_t); }
+size_t rtn_out_addr6_bytes(uint32_t n) { return (size_t)((n + 63u) / 64u) * 64u * 32u; }
+size_t rtn_out_dlv_bytes(uint32_t n, uint32_t deliver_words) {
+  return (size_t)((n + 63u) / 64u) * 64u * (1u + deliver_words) * 8u;
+}
+
+}  // extern "C"

@@ -1,0 +1,273 @@
+"""ctypes binding of the C ABI in include/retina_pc.h (libretina_pc.so, built in-tree).
+
+This is the host-side mirror used by tests, bench.py and the Python Subscription shim; the
+product path is the HIP kernel behind rtn_pc_run. There is no CPU fallback: if the shared
+library or a GPU is missing, these calls raise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from pathlib import Path
+
+import numpy as np
+
+_LIB_PATH = Path(__file__).resolve().parent / "_lib" / "libretina_pc.so"
+_lib = None
+
+RTN_OK = 0
+
+
+class RetinaError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"[{code}] {msg}")
+        self.code = code
+
+
+class FilterError(RetinaError):
+    """The subscription/filter would be rejected by the reference's filtergen."""
+
+
+class _Batch(C.Structure):
+    _fields_ = [("slab", C.c_void_p), ("stride", C.c_uint64), ("data_len", C.c_void_p),
+                ("n", C.c_uint32), ("core_id", C.c_uint32)]
+
+
+class _Out(C.Structure):
+    _fields_ = [("pc_bitmap", C.c_void_p), ("fwd_bitmap", C.c_void_p), ("l4", C.c_void_p),
+                ("addr6", C.c_void_p), ("dlv_bitmap", C.c_void_p), ("dlv_records", C.c_void_p),
+                ("counters", C.c_void_p)]
+
+
+class _Info(C.Structure):
+    _fields_ = [("n_subscriptions", C.c_uint32), ("n_deliver_stmts", C.c_uint32),
+                ("deliver_words", C.c_uint32), ("tree_size", C.c_uint32)]
+
+
+EXPORTS = {
+    "rtn_last_error": (C.c_char_p, []),
+    "rtn_program_compile": (C.c_int32, [C.c_char_p, C.c_size_t, C.POINTER(C.c_void_p)]),
+    "rtn_program_compile_filter": (C.c_int32, [C.c_char_p, C.c_char_p, C.c_char_p, C.POINTER(C.c_void_p)]),
+    "rtn_program_info": (C.c_int32, [C.c_void_p, C.POINTER(_Info)]),
+    "rtn_program_tree": (C.c_size_t, [C.c_void_p, C.c_char_p, C.c_size_t]),
+    "rtn_program_rust": (C.c_size_t, [C.c_void_p, C.c_char_p, C.c_size_t]),
+    "rtn_program_source": (C.c_size_t, [C.c_void_p, C.c_char_p, C.c_size_t]),
+    "rtn_program_deliver_table": (C.c_int32, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32]),
+    "rtn_program_code_object": (C.c_int32, [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]),
+    "rtn_program_destroy": (None, [C.c_void_p]),
+    "rtn_pc_create": (C.c_int32, [C.c_char_p, C.c_size_t, C.c_int, C.POINTER(C.c_void_p)]),
+    "rtn_pc_create_from_program": (C.c_int32, [C.c_void_p, C.c_int, C.POINTER(C.c_void_p)]),
+    "rtn_pc_run": (C.c_int32, [C.c_void_p, C.POINTER(_Batch), C.POINTER(_Out), C.c_void_p]),
+    "rtn_pc_set_grid": (C.c_int32, [C.c_void_p, C.c_uint32]),
+    "rtn_pc_destroy": (C.c_int32, [C.c_void_p]),
+    "rtn_out_bitmap_bytes": (C.c_size_t, [C.c_uint32]),
+    "rtn_out_l4_bytes": (C.c_size_t, [C.c_uint32]),
+    "rtn_out_addr6_bytes": (C.c_size_t, [C.c_uint32]),
+    "rtn_out_dlv_bytes": (C.c_size_t, [C.c_uint32, C.c_uint32]),
+}
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not _LIB_PATH.exists():
+            raise RetinaError(-2, f"{_LIB_PATH} not built (run __graft_entry__.build())")
+        L = C.CDLL(str(_LIB_PATH))
+        for name, (res, args) in EXPORTS.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _check(rc: int) -> None:
+    if rc != RTN_OK:
+        msg = lib().rtn_last_error().decode(errors="replace")
+        raise (FilterError if rc == -74 else RetinaError)(rc, msg)
+
+
+def _text(fn, h) -> str:
+    n = fn(h, None, 0)
+    buf = C.create_string_buffer(n + 1)
+    fn(h, buf, n + 1)
+    return buf.value.decode()
+
+
+L4_DTYPE = np.dtype([("pkt_idx", "<u4"), ("src_ip4", "<u4"), ("dst_ip4", "<u4"), ("ports", "<u4"),
+                     ("seq_no", "<u4"), ("ack_no", "<u4"), ("off_len", "<u4"), ("proto_flags", "<u4")])
+
+
+class Program:
+    """A compiled subscription set (the output of filtergen for the packet stage)."""
+
+    def __init__(self, handle: int):
+        self._h = C.c_void_p(handle)
+
+    @classmethod
+    def from_spec(cls, toml_text: str) -> "Program":
+        h = C.c_void_p()
+        b = toml_text.encode()
+        _check(lib().rtn_program_compile(b, len(b), C.byref(h)))
+        return cls(h.value)
+
+    @classmethod
+    def from_filter(cls, filter_str: str, datatypes=("ConnRecord",), callback: str = "cb") -> "Program":
+        h = C.c_void_p()
+        _check(lib().rtn_program_compile_filter(filter_str.encode(), ",".join(datatypes).encode(),
+                                                callback.encode(), C.byref(h)))
+        return cls(h.value)
+
+    def __del__(self):
+        if getattr(self, "_h", None) and self._h.value and _lib is not None:
+            _lib.rtn_program_destroy(self._h)
+            self._h = C.c_void_p()
+
+    @property
+    def info(self) -> dict:
+        i = _Info()
+        _check(lib().rtn_program_info(self._h, C.byref(i)))
+        return {f: getattr(i, f) for f, _ in _Info._fields_}
+
+    @property
+    def tree(self) -> str:
+        return _text(lib().rtn_program_tree, self._h)
+
+    @property
+    def rust(self) -> str:
+        return _text(lib().rtn_program_rust, self._h)
+
+    @property
+    def source(self) -> str:
+        return _text(lib().rtn_program_source, self._h)
+
+    def deliver_table(self) -> tuple[np.ndarray, np.ndarray]:
+        n = self.info["n_deliver_stmts"]
+        subs = np.zeros(max(n, 1), np.uint32)
+        pay = np.zeros(max(n, 1), np.uint8)
+        _check(lib().rtn_program_deliver_table(self._h, subs.ctypes.data, pay.ctypes.data, max(n, 1)))
+        return subs[:n], pay[:n]
+
+    def code_object(self) -> bytes:
+        p = C.c_void_p()
+        n = C.c_size_t()
+        _check(lib().rtn_program_code_object(self._h, C.byref(p), C.byref(n)))
+        return C.string_at(p, n.value)
+
+
+@dataclass
+class PCOutputs:
+    """Device-side output buffers (torch tensors) of one rtn_pc_run."""
+    n: int
+    pc_bitmap: object
+    fwd_bitmap: object
+    l4: object
+    addr6: object
+    dlv_bitmap: object
+    dlv_records: object
+    counters: object
+    deliver_words: int
+
+    def counters_host(self) -> np.ndarray:
+        return self.counters.cpu().numpy().view(np.uint32)
+
+    def decode(self) -> dict:
+        """Bring results to the host in frame order (numpy)."""
+        n = self.n
+        pc_bm = self.pc_bitmap.cpu().numpy().view(np.uint64)
+        fwd_bm = self.fwd_bitmap.cpu().numpy().view(np.uint64)
+        pc = np.unpackbits(pc_bm.view(np.uint8), bitorder="little")[:n].astype(bool)
+        fwd = np.unpackbits(fwd_bm.view(np.uint8), bitorder="little")[:n].astype(bool)
+        recs_all = self.l4.cpu().numpy().view(L4_DTYPE)
+        idx = _segment_index(fwd_bm)
+        recs = recs_all[idx]
+        out = {"pc": pc, "fwd": fwd, "l4": recs}
+        if self.addr6 is not None:
+            a6 = self.addr6.cpu().numpy().view(np.uint8).reshape(-1, 32)
+            out["addr6"] = a6[idx]
+        if self.deliver_words:
+            dbm = self.dlv_bitmap.cpu().numpy().view(np.uint64)
+            recs_d = self.dlv_records.cpu().numpy().view(np.uint64).reshape(-1, 1 + self.deliver_words)
+            di = _segment_index(dbm)
+            out["dlv"] = recs_d[di]
+        return out
+
+
+def _segment_index(bm: np.ndarray) -> np.ndarray:
+    counts = np.unpackbits(bm.view(np.uint8), bitorder="little").reshape(-1, 64).sum(1).astype(np.int64)
+    total = int(counts.sum())
+    if total == 0:
+        return np.zeros(0, np.int64)
+    starts = np.repeat(np.arange(len(bm), dtype=np.int64) * 64, counts)
+    first = np.repeat(np.cumsum(counts) - counts, counts)
+    return starts + (np.arange(total, dtype=np.int64) - first)
+
+
+class PacketContinue:
+    """A Program loaded on one GPU: batch version of Subscription::continue_packet plus the
+    L4Context gate of process_packet (core/src/subscription/mod.rs:94-127)."""
+
+    def __init__(self, program: Program, device: int = 0):
+        self.program = program
+        self.device = device
+        h = C.c_void_p()
+        _check(lib().rtn_pc_create_from_program(program._h, device, C.byref(h)))
+        self._h = h
+        self.deliver_words = program.info["deliver_words"]
+
+    def __del__(self):
+        if getattr(self, "_h", None) and self._h.value and _lib is not None:
+            _lib.rtn_pc_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def set_grid(self, blocks: int) -> None:
+        _check(lib().rtn_pc_set_grid(self._h, blocks))
+
+    def alloc_outputs(self, n: int, addr6: bool = True, counters: bool = True) -> PCOutputs:
+        import torch
+
+        dev = torch.device("cuda", self.device)
+        L = lib()
+        u8 = lambda nbytes: torch.empty(nbytes, dtype=torch.uint8, device=dev)  # noqa: E731
+        dw = self.deliver_words
+        return PCOutputs(
+            n=n,
+            pc_bitmap=u8(L.rtn_out_bitmap_bytes(n)),
+            fwd_bitmap=u8(L.rtn_out_bitmap_bytes(n)),
+            l4=u8(L.rtn_out_l4_bytes(n)),
+            addr6=u8(L.rtn_out_addr6_bytes(n)) if addr6 else None,
+            dlv_bitmap=u8(L.rtn_out_bitmap_bytes(n)) if dw else None,
+            dlv_records=u8(L.rtn_out_dlv_bytes(n, dw)) if dw else None,
+            counters=torch.zeros(16, dtype=torch.uint8, device=dev) if counters else None,
+            deliver_words=dw,
+        )
+
+    def run(self, slab, stride: int, data_len, n: int | None = None, out: PCOutputs | None = None,
+            stream=None, core_id: int = 0) -> PCOutputs:
+        import torch
+
+        if n is None:
+            n = int(data_len.numel())
+        if out is None or out.n < n:
+            out = self.alloc_outputs(n)
+        b = _Batch(slab.data_ptr(), stride, data_len.data_ptr(), n, core_id)
+        ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
+        o = _Out(ptr(out.pc_bitmap), ptr(out.fwd_bitmap), ptr(out.l4), ptr(out.addr6), ptr(out.dlv_bitmap),
+                 ptr(out.dlv_records), ptr(out.counters))
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        _check(lib().rtn_pc_run(self._h, C.byref(b), C.byref(o), C.c_void_p(s.cuda_stream)))
+        out.n = n
+        return out
+
+
+def pack_frames(frames, stride: int = 128) -> tuple[np.ndarray, np.ndarray]:
+    """Lay frames out as a header slab (slot = first min(len, stride) bytes) + u16 data_len."""
+    n = len(frames)
+    slab = np.zeros((n, stride), np.uint8)
+    dlen = np.zeros(n, np.uint16)
+    for i, f in enumerate(frames):
+        b = np.frombuffer(bytes(f), np.uint8)
+        k = min(len(b), stride)
+        slab[i, :k] = b[:k]
+        dlen[i] = len(b)
+    return slab.reshape(-1), dlen
