@@ -1,0 +1,99 @@
+"""Shared test helpers: run the product (GPU, through the C ABI) and the oracle (CPU) on the same
+frames and bring both to one canonical per-frame form."""
+from __future__ import annotations
+
+import numpy as np
+
+from oracle import cgen, filterlang
+
+# canonical per-forwarded-frame record
+REC = np.dtype([("idx", "<u8"), ("ver", "<u4"), ("proto", "<u4"), ("sport", "<u4"), ("dport", "<u4"),
+                ("offset", "<u4"), ("length", "<u4"), ("seq", "<u4"), ("ack", "<u4"), ("flags", "<u4"),
+                ("src", "u1", 16), ("dst", "u1", 16)])
+
+
+def subs_from_spec(spec: str) -> list[filterlang.Sub]:
+    return filterlang.load_spec(spec)
+
+
+_ORACLES: dict[str, cgen.OracleLib] = {}
+
+
+def oracle_lib(spec: str) -> cgen.OracleLib:
+    if spec not in _ORACLES:
+        _ORACLES[spec] = cgen.OracleLib(filterlang.PacketTree(subs_from_spec(spec)))
+    return _ORACLES[spec]
+
+
+def oracle_run(spec: str, slab: np.ndarray, stride: int, dlen: np.ndarray) -> dict:
+    lib = oracle_lib(spec)
+    r = lib.eval(slab, stride, dlen)
+    idx = np.nonzero(r["fwd"])[0]
+    src = r["l4"][idx]
+    rec = np.zeros(len(idx), REC)
+    rec["idx"] = idx
+    for f in ("ver", "proto", "sport", "dport", "offset", "length", "seq", "ack", "flags"):
+        rec[f] = src[f]
+    rec["src"] = src["src"]
+    rec["dst"] = src["dst"]
+    return {"pc": r["pc"], "fwd": r["fwd"], "rec": rec, "dm": r["dm"]}
+
+
+def gpu_run(spec: str, slab: np.ndarray, stride: int, dlen: np.ndarray, device: int = 0) -> dict:
+    import torch
+
+    from retina_amd import pc
+
+    prog = pc.Program.from_spec(spec)
+    ctx = pc.PacketContinue(prog, device)
+    dev = torch.device("cuda", device)
+    n = len(dlen)
+    slab_t = torch.from_numpy(np.ascontiguousarray(slab, np.uint8)).to(dev)
+    dl_t = torch.from_numpy(np.ascontiguousarray(dlen, np.uint16).view(np.int16)).to(dev)
+    out = ctx.run(slab_t, stride, dl_t, n)
+    torch.cuda.synchronize()
+    d = out.decode()
+    cnt = out.counters_host()
+    l4 = d["l4"]
+    rec = np.zeros(len(l4), REC)
+    rec["idx"] = l4["pkt_idx"]
+    rec["ver"] = (l4["proto_flags"] >> 16) & 0xFF
+    rec["proto"] = l4["proto_flags"] & 0xFF
+    rec["flags"] = (l4["proto_flags"] >> 8) & 0xFF
+    rec["sport"] = l4["ports"] & 0xFFFF
+    rec["dport"] = l4["ports"] >> 16
+    rec["offset"] = l4["off_len"] & 0xFFFF
+    rec["length"] = l4["off_len"] >> 16
+    rec["seq"] = l4["seq_no"]
+    rec["ack"] = l4["ack_no"]
+    v4 = rec["ver"] == 4
+    rec["src"][v4, :4] = l4["src_ip4"][v4].astype(">u4").view(np.uint8).reshape(-1, 4)
+    rec["dst"][v4, :4] = l4["dst_ip4"][v4].astype(">u4").view(np.uint8).reshape(-1, 4)
+    a6 = d["addr6"]
+    rec["src"][~v4] = a6[~v4, :16]
+    rec["dst"][~v4] = a6[~v4, 16:]
+    nd = prog.info["deliver_words"]
+    dm = np.zeros((n, nd), np.uint64)
+    if nd:
+        dl = d["dlv"]
+        dm[dl[:, 0].astype(np.int64)] = dl[:, 1:]
+    return {"pc": d["pc"], "fwd": d["fwd"], "rec": rec, "dm": dm, "counters": cnt, "program": prog}
+
+
+def assert_same(gpu: dict, ora: dict, what: str = "") -> None:
+    n = len(ora["pc"])
+    bad = np.nonzero(gpu["pc"] != ora["pc"])[0]
+    assert bad.size == 0, f"{what}: PacketContinue differs at {bad[:10]} ({bad.size} of {n})"
+    bad = np.nonzero(gpu["fwd"] != ora["fwd"])[0]
+    assert bad.size == 0, f"{what}: forwarded set differs at {bad[:10]} ({bad.size} of {n})"
+    g, o = gpu["rec"], ora["rec"]
+    assert len(g) == len(o), f"{what}: {len(g)} vs {len(o)} L4Context records"
+    for f in REC.names:
+        if not np.array_equal(g[f], o[f]):
+            k = np.nonzero((g[f] != o[f]).reshape(len(g), -1).any(1))[0][:5]
+            raise AssertionError(f"{what}: L4Context field {f} differs at records {k}: {g[k]} vs {o[k]}")
+    assert np.array_equal(gpu["dm"], ora["dm"]), f"{what}: packet-level deliveries differ"
+    if "counters" in gpu:
+        c = gpu["counters"]
+        assert c[0] == ora["pc"].sum() and c[1] == ora["fwd"].sum(), f"{what}: counters {c}"
+        assert c[2] == int((ora["dm"] != 0).any(1).sum()) if ora["dm"].size else c[2] == 0

@@ -1,0 +1,69 @@
+"""The C-ABI library: loads on a machine without a GPU, exports every function declared in
+include/retina_pc.h, reports errors the way the header says, and its hiprtc path produces a
+gfx950 code object for every named subscription set (no GPU needed to compile)."""
+from __future__ import annotations
+
+import ctypes as C
+import re
+from pathlib import Path
+
+import pytest
+
+from golden.filter_sets import SETS
+from retina_amd import pc
+
+HEADER = Path(__file__).resolve().parent.parent / "include" / "retina_pc.h"
+
+
+def declared_functions() -> list[str]:
+    text = HEADER.read_text()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(rtn_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_exports_every_declared_symbol():
+    lib = C.CDLL(str(pc._LIB_PATH))
+    names = declared_functions()
+    assert len(names) >= 18
+    for n in names:
+        assert hasattr(lib, n), n
+    assert set(names) == set(pc.EXPORTS), set(names) ^ set(pc.EXPORTS)
+
+
+def test_error_codes_and_messages():
+    with pytest.raises(pc.FilterError) as e:
+        pc.Program.from_filter("tcp.dst_port = 99999", ["ConnRecord"])
+    assert e.value.code == -74 and "out of range" in str(e.value)
+    with pytest.raises(pc.FilterError):
+        pc.Program.from_spec("[[subscriptions]]\nfilter = \"tcp\"\ndatatypes = [\"NoSuchType\"]\ncallback = \"x\"\n")
+    with pytest.raises(pc.FilterError):
+        pc.Program.from_spec("[[subscriptions]]\nfilter = \"tcp\"\ndatatypes = [\"ZcFrame\", \"ConnRecord\"]\ncallback = \"x\"\n")
+    with pytest.raises(pc.FilterError):
+        pc.Program.from_spec("[[subscriptions]]\nfilter = \"tcp\"\ndatatypes = [\"ZcFrame\", \"FiveTuple\"]\ncallback = \"x\"\n")
+    L = pc.lib()
+    assert L.rtn_pc_run(None, None, None, None) == -22
+    assert L.rtn_program_info(None, None) == -22
+    assert b"null" in L.rtn_last_error()
+
+
+def test_program_text_outputs():
+    p = pc.Program.from_spec(SETS["cfg2"])
+    assert p.info == {"n_subscriptions": 1, "n_deliver_stmts": 0, "deliver_words": 0, "tree_size": 7}
+    assert "tcp.dst_port = 80" in p.tree
+    assert "if tcp.dst_port() == 80 {" in p.rust
+    assert "rtn_pc_kernel" in p.source and "RTN_DELIVER_WORDS 0" in p.source
+
+
+@pytest.mark.parametrize("fset", list(SETS))
+def test_hiprtc_builds_gfx950_code_object(fset):
+    co = pc.Program.from_spec(SETS[fset]).code_object()
+    assert len(co) > 1000
+    assert b"gfx950" in co or co[:4] == b"\x7fELF" or co[:24].startswith(b"__CLANG_OFFLOAD_BUNDLE__")
+
+
+def test_output_sizes():
+    L = pc.lib()
+    assert L.rtn_out_bitmap_bytes(65) == 16
+    assert L.rtn_out_l4_bytes(65) == 128 * 32
+    assert L.rtn_out_addr6_bytes(1) == 64 * 32
+    assert L.rtn_out_dlv_bytes(64, 2) == 64 * 3 * 8

@@ -1,0 +1,144 @@
+"""CPU tests of the oracle: it reproduces the committed golden fixtures, its two restatements
+(pure Python vs generated C) agree, and its independent compiler agrees with the product's C++
+compiler (tree shape, else-if marking, callback statement order) on the reference's filters."""
+from __future__ import annotations
+
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+import helpers
+from golden.filter_sets import SETS
+from oracle import filterlang, packet, pcap
+from retina_amd import pc, synth
+
+GOLD = Path(__file__).resolve().parent / "golden"
+
+
+def _corpus(name):
+    if name == "traces":
+        t = np.load(GOLD / "traces.npz")
+        return t["slab"], t["dlen"]
+    t = np.load(GOLD / "corpus_adversarial.npz")
+    return t["slab"], t["dlen"]
+
+
+@pytest.mark.parametrize("corpus", ["traces", "adversarial"])
+@pytest.mark.parametrize("fset", list(SETS))
+def test_c_oracle_reproduces_golden(fset, corpus):
+    g = np.load(GOLD / f"golden_{fset}.npz")
+    slab, dlen = _corpus(corpus)
+    r = helpers.oracle_run(SETS[fset], slab, 128, dlen)
+    n = len(dlen)
+    assert np.array_equal(r["pc"], np.unpackbits(g[f"{corpus}_pc"])[:n].astype(bool))
+    assert np.array_equal(r["fwd"], np.unpackbits(g[f"{corpus}_fwd"])[:n].astype(bool))
+    assert np.array_equal(r["rec"], g[f"{corpus}_rec"])
+    assert np.array_equal(r["dm"], g[f"{corpus}_dm"])
+
+
+@pytest.mark.parametrize("fset", ["cfg3", "quirks", "payload", "match_all"])
+def test_python_oracle_matches_golden(fset):
+    """Independent restatement (oracle/packet.py) against the fixture, frame by frame."""
+    g = np.load(GOLD / f"golden_{fset}.npz")
+    slab, dlen = _corpus("adversarial")
+    tree = filterlang.PacketTree(filterlang.load_spec(SETS[fset]))
+    pcb = np.unpackbits(g["adversarial_pc"])
+    dm = g["adversarial_dm"]
+    b = slab.reshape(-1, 128)
+    for i in range(0, len(dlen), 3):
+        act, fired = packet.evaluate(tree, b[i].tobytes(), int(dlen[i]))
+        assert bool(act & 1) == bool(pcb[i])
+        m = 0
+        for k in fired:
+            m |= 1 << k
+        assert m == (int(dm[i, 0]) if dm.shape[1] else 0)
+
+
+def test_traces_fixture_matches_pcaps(reference_dir):
+    """traces.npz is exactly what offline.rs would hand to continue_packet."""
+    t = np.load(GOLD / "traces.npz")
+    frames = []
+    for name in t["names"]:
+        frames += pcap.offline_frames(reference_dir / "traces" / str(name), mtu=9702)
+    slab, dlen = pc.pack_frames(frames, 128)
+    assert np.array_equal(slab, t["slab"]) and np.array_equal(dlen, t["dlen"])
+
+
+def test_l4context_examples():
+    """Hand-checked L4Context values (pdu.rs:86-171) including the checked_sub underflow."""
+    import corpus as C
+
+    t = C.tcp(sport=1111, dport=2222, seq=7, ack=9, flags=0x12, payload=b"abcd")
+    f = C.eth(0x0800) + C.ipv4(6, len(t)) + t
+    c = packet.l4context(f, len(f))
+    assert (c.sport, c.dport, c.proto, c.offset, c.length, c.seq, c.ack, c.flags) == (1111, 2222, 6, 54, 4, 7, 9, 0x12)
+    f = C.eth(0x0800) + C.ipv4(6, 0, total=39) + t
+    assert packet.l4context(f, len(f)) is None
+    u = C.udp(payload=b"xyz")
+    f = C.eth(0x86DD, vlan=4) + C.ipv6(17, len(u)) + u
+    c = packet.l4context(f, len(f))
+    assert (c.ver, c.proto, c.offset, c.length) == (6, 17, 18 + 40 + 8, 3)
+    f = C.eth(0x0800) + C.ipv4(6, len(t), ihl=2) + t   # IHL 2: L4 inside the IPv4 header
+    c = packet.l4context(f, len(f))
+    assert c is not None and c.offset == 22 + ((f[34] & 0xF0) >> 2)
+
+
+FILTERS = [
+    "tcp.dst_port = 80", "tls", "dns", "ipv4", "ipv6 and udp", "tcp.port != 80", "ipv4.addr = 1.1.1.1",
+    "tcp.port in 80..90 or udp.dst_port >= 53", "ipv4.src_addr in 10.0.0.0/8 and tcp.syn = 1",
+    "ipv6.dst_addr = ::1 or ipv6.src_addr = fe80::/10", "(tcp or udp) and ipv4.time_to_live < 3",
+    "http.uri = '/x' and tcp.dst_port = 8080", "quic and udp.port != 443", "tcp.flags = 2 or tcp.flags = 18",
+    "ipv4.protocol = 1", "udp.length > 100 and udp.dst_port = 1434", "",
+]
+
+
+@pytest.mark.parametrize("dts", [["ConnRecord"], ["ZcFrame", "FilterStr"], ["Payload"], ["TlsHandshake"]])
+@pytest.mark.parametrize("flt", FILTERS)
+def test_compilers_agree_single(flt, dts):
+    if "TlsHandshake" in dts and "tls" not in flt:
+        dts = ["ConnRecord"]
+    prod = pc.Program.from_filter(flt, dts)
+    ora = filterlang.PacketTree([filterlang.Sub(flt, dts)])
+    assert prod.tree == ora.pprint()
+    subs, pay = prod.deliver_table()
+    st = packet.statement_table(ora)
+    assert [s for s, _ in st] == list(subs)
+    assert [k == "Payload" for _, k in st] == [bool(x) for x in pay]
+
+
+@pytest.mark.parametrize("fset", list(SETS))
+def test_compilers_agree_sets(fset):
+    prod = pc.Program.from_spec(SETS[fset])
+    ora = filterlang.PacketTree(filterlang.load_spec(SETS[fset]))
+    assert prod.tree == ora.pprint()
+
+
+def test_compilers_agree_filter_stats(reference_dir):
+    """The reference's largest subscription file (1575 subscriptions, mostly L7) compiles to the
+    same PacketContinue tree in both compilers."""
+    text = (reference_dir / "examples/filter_stats/spec.toml").read_text()
+    prod = pc.Program.from_spec(text)
+    ora = filterlang.PacketTree(filterlang.load_spec(text))
+    assert prod.tree == ora.pprint()
+    assert prod.info["n_subscriptions"] == 1575
+
+
+BAD = ["tcp.dst_port = 70000", "ipv4 and ipv6", "ipv4.rf = 1", "tcp.port in 90..80", "ipv4.src_addr = 1.2.3.256",
+       "ipv4.src_addr = 1.2.3.4/33", "tcp.foo = 1", "tcp and", "(tcp", "tcp.dst_port = 'x'", "ethernet",
+       "ipv4.src_addr = 01.2.3.4", "tcp.dst_port in 5", "ipv6.src_addr = 1.2.3.4", "ipv4.src_addr = ::1", "bogus"]
+
+
+@pytest.mark.parametrize("flt", BAD)
+def test_both_compilers_reject(flt):
+    with pytest.raises(pc.FilterError):
+        pc.Program.from_filter(flt, ["ConnRecord"])
+    with pytest.raises(Exception):
+        t = filterlang.PacketTree([filterlang.Sub(flt, ["ConnRecord"])])
+        from oracle import cgen
+        cgen.generate_c(t)
+
+
+def test_synth_alg_bytes():
+    s, d = synth.cfg2(1000)
+    assert synth.alg_read_bytes(s, d, 64) == 66 * 1000
