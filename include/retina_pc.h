@@ -75,7 +75,8 @@ typedef struct rtn_pc_out {
   uint8_t* addr6;        /* optional [ceil(n/64)*64][32]: IPv6 src|dst bytes of IPv6 records  */
   uint64_t* dlv_bitmap;  /* [ceil(n/64)] frames with >= 1 packet-level callback (if any)     */
   uint64_t* dlv_records; /* [ceil(n/64)*64][1 + deliver_words]: frame index, statement mask  */
-  uint32_t* counters;    /* optional [4]: pc, fwd, dlv totals, status bits; zeroed per run   */
+  uint32_t* counters;    /* optional [4]: pc, fwd, dlv totals, status bits; zeroed per run
+                          (NULL: no totals, no memset -- the run is a single kernel launch) */
 } rtn_pc_out_t;
 
 typedef struct rtn_program_info {

@@ -44,7 +44,7 @@ struct rtn_args {
   rtn_u64 stride;
   const unsigned short* dlen;
   rtn_u32 n;
-  rtn_u32 flags;              // bit0: write addr6 side array
+  rtn_u32 flags;              // bit0: write addr6 side array, bit1: accumulate counters
   rtn_u64* pc_bm;             // [ceil(n/64)]  PacketContinue bit
   rtn_u64* fwd_bm;            // [ceil(n/64)]  PacketContinue && L4Context::new Ok
   rtn_l4rec* recs;            // [ceil(n/64)*64]
@@ -253,6 +253,7 @@ extern "C" __global__ void __launch_bounds__(256) rtn_pc_kernel(rtn_args a) {
 #endif
   }
   // one set of atomics per wave
+  if (!(a.flags & 2u)) return;
   if (lane == 0u) {
     if (c_pc) atomicAdd(&a.counters[0], c_pc);
     if (c_fwd) atomicAdd(&a.counters[1], c_fwd);

@@ -272,22 +272,24 @@ int32_t rtn_pc_run(rtn_pc_t* pc, const rtn_batch_t* in, rtn_pc_out_t* out, void*
   if (dw > 0 && (!out->dlv_bitmap || !out->dlv_records))
     return fail(RTN_EINVAL, "program has packet-level callbacks: dlv_bitmap/dlv_records required");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  uint32_t* counters = out->counters ? out->counters : pc->scratch_counters;
-  hipError_t e = hipMemsetAsync(counters, 0, 16, s);
-  if (e != hipSuccess) return fail(RTN_EDEVICE, std::string("hipMemsetAsync: ") + hipGetErrorString(e));
+  hipError_t e;
+  if (out->counters) {
+    e = hipMemsetAsync(out->counters, 0, 16, s);
+    if (e != hipSuccess) return fail(RTN_EDEVICE, std::string("hipMemsetAsync: ") + hipGetErrorString(e));
+  }
   KArgs a;
   a.slab = in->slab;
   a.stride = in->stride;
   a.dlen = in->data_len;
   a.n = in->n;
-  a.flags = out->addr6 ? 1u : 0u;
+  a.flags = (out->addr6 ? 1u : 0u) | (out->counters ? 2u : 0u);
   a.pc_bm = out->pc_bitmap;
   a.fwd_bm = out->fwd_bitmap;
   a.recs = out->l4;
   a.addr6 = out->addr6;
   a.dlv_bm = out->dlv_bitmap;
   a.dlv_recs = out->dlv_records;
-  a.counters = counters;
+  a.counters = out->counters ? out->counters : pc->scratch_counters;
   const uint32_t groups = (in->n + 63u) / 64u;
   uint32_t blocks = pc->blocks ? pc->blocks : 2048u;
   const uint32_t need = (groups + 3u) / 4u;

@@ -1,0 +1,56 @@
+"""Summarise rocprofv3 outputs into profiles/ (committed evidence for bench.py's roofline block).
+
+    python scripts/pmc_summary.py <tag> <cfg> <frames>
+
+Reads gpurun_out/prof_<tag>_<cfg>/run_kernel_stats.csv (kernel-trace --stats pass) and
+gpurun_out/pmc_<tag>_<cfg>_{FETCH_SIZE,WRITE_SIZE}/run_counter_collection.csv (separate --pmc
+passes) and writes profiles/<tag>_<cfg>_kernel_stats.csv and profiles/pmc_<cfg>.json.
+HBM bytes per launch = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024: FETCH_SIZE/WRITE_SIZE are in KiB
+and gfx950 reports exactly half the bytes of a wide coalesced read in FETCH_SIZE
+(MI355X_MICROARCH.md §HBM); WRITE_SIZE is exact for 16-B-per-lane stores.
+"""
+from __future__ import annotations
+
+import csv
+import json
+import shutil
+import statistics
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+KERNEL = "rtn_pc_kernel"
+
+
+def counter(path: Path) -> list[float]:
+    rows = list(csv.DictReader(open(path)))
+    return [float(r["Counter_Value"]) for r in rows if KERNEL in r.get("Kernel_Name", "")]
+
+
+def main(tag: str, cfg: str, frames: int) -> None:
+    out = ROOT / "gpurun_out"
+    prof = ROOT / "profiles"
+    prof.mkdir(exist_ok=True)
+    ks = out / f"prof_{tag}_{cfg}" / "run_kernel_stats.csv"
+    shutil.copy(ks, prof / f"{tag}_{cfg}_kernel_stats.csv")
+    stats = {r["Name"]: r for r in csv.DictReader(open(ks))}
+    k = stats[KERNEL]
+    fetch = counter(out / f"pmc_{tag}_{cfg}_FETCH_SIZE" / "run_counter_collection.csv")
+    write = counter(out / f"pmc_{tag}_{cfg}_WRITE_SIZE" / "run_counter_collection.csv")
+    f_kb, w_kb = statistics.median(fetch), statistics.median(write)
+    d = {
+        "tag": tag, "config": cfg, "frames": frames, "kernel": KERNEL,
+        "kernel_avg_ns": float(k["AverageNs"]), "kernel_calls": int(k["Calls"]),
+        "fetch_size_kib_median": f_kb, "write_size_kib_median": w_kb, "pmc_dispatches": [len(fetch), len(write)],
+        "read_bytes_per_launch": int(2 * f_kb * 1024), "write_bytes_per_launch": int(w_kb * 1024),
+        "hbm_bytes_per_launch": int(2 * f_kb * 1024 + w_kb * 1024),
+        "correction": "read = 2 x FETCH_SIZE KiB (gfx950 half-count of wide coalesced reads); write = WRITE_SIZE KiB",
+        "source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes; kernel stats from "
+                  f"rocprofv3 --kernel-trace --stats ({tag})",
+    }
+    (prof / f"pmc_{cfg}.json").write_text(json.dumps(d, indent=2) + "\n")
+    print(json.dumps(d, indent=2))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2], int(sys.argv[3]))
