@@ -22,6 +22,7 @@
 
 typedef unsigned int rtn_u32;
 typedef unsigned long long rtn_u64;
+typedef unsigned int rtn_v4u __attribute__((ext_vector_type(4)));
 
 #ifndef RTN_DELIVER_WORDS
 #define RTN_DELIVER_WORDS 0
@@ -147,118 +148,251 @@ __device__ __forceinline__ void rtn_parse(const rtn_u32 (&w)[32], rtn_u32 dl, rt
   v.payload_ok = v.l4ok && off < dl && off + len <= dl;
 }
 
+struct rtn_acc {
+  rtn_u32 pc, fwd, dlv, status;
+};
+
+// Load the first 64 B of frame i's slot (the only part a 64-B-stride batch has).
+__device__ __forceinline__ void rtn_load_lo(const rtn_args& a, rtn_u32 i, bool valid, rtn_u32 (&lo)[16], rtn_u32& dl) {
+  dl = 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) lo[k] = 0u;
+  if (valid) {
+    const uint4* slot = reinterpret_cast<const uint4*>(a.slab + (rtn_u64)i * a.stride);
+    dl = a.dlen[i];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint4 x = slot[k];
+      lo[4 * k + 0] = x.x; lo[4 * k + 1] = x.y; lo[4 * k + 2] = x.z; lo[4 * k + 3] = x.w;
+    }
+  }
+}
+
+// Coalesced variant: 4 lanes per slot read the slot's first 64 B (each wave instruction covers
+// 16 slots), then a wave-private LDS tile (80-B pitch: conflict-free ds_read_b128) turns it back
+// into one frame per lane.
+#define RTN_XPITCH 20u  // dwords per frame in the LDS tile
+__device__ __forceinline__ void rtn_load_raw(const rtn_args& a, rtn_u32 wv, rtn_u32 lane, uint4 (&q)[4], rtn_u32& dl) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const rtn_u32 p = wv * 64u + 16u * k + (lane >> 2);
+    q[k] = make_uint4(0u, 0u, 0u, 0u);
+    if (p < a.n) q[k] = *reinterpret_cast<const uint4*>(a.slab + (rtn_u64)p * a.stride + (lane & 3u) * 16u);
+  }
+  const rtn_u32 i = wv * 64u + lane;
+  dl = i < a.n ? (rtn_u32)a.dlen[i] : 0u;
+}
+__device__ __forceinline__ void rtn_xpose(rtn_u32* tile, rtn_u32 lane, const uint4 (&q)[4], rtn_u32 (&lo)[16]) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    *reinterpret_cast<uint4*>(tile + (16u * k + (lane >> 2)) * RTN_XPITCH + (lane & 3u) * 4u) = q[k];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint4 x = *reinterpret_cast<const uint4*>(tile + lane * RTN_XPITCH + 4u * j);
+    lo[4 * j + 0] = x.x; lo[4 * j + 1] = x.y; lo[4 * j + 2] = x.z; lo[4 * j + 3] = x.w;
+  }
+}
+
+// Everything after the first 64 B arrived: optional second 64 B, parse, generated filter,
+// L4Context, wave-level compaction of the outputs of group wv.
+__device__ __forceinline__ void rtn_group(const rtn_args& a, rtn_u32 wv, rtn_u32 lane, rtn_u64 lane_lt,
+                                          const rtn_u32 (&lo)[16], rtn_u32 dl, rtn_acc& acc) {
+  const rtn_u32 i = wv * 64u + lane;
+  const bool valid = i < a.n;
+  rtn_u32 w[32];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) w[k] = lo[k];
+#pragma unroll
+  for (int k = 16; k < 32; ++k) w[k] = 0u;
+  // Second 64 B only where a header can reach past byte 64 (IPv6, IPv4 options, VLAN+options).
+  {
+    const rtn_u32 et = ((w[3] & 0xffu) << 8) | ((w[3] >> 8) & 0xffu);
+    const rtn_u32 l3 = et == 0x8100u ? 18u : 14u;
+    const rtn_u32 vihl = l3 == 18u ? (w[4] >> 16) & 0xffu : (w[3] >> 16) & 0xffu;
+    const rtn_u32 inner = et == 0x8100u ? (((w[4] & 0xffu) << 8) | ((w[4] >> 8) & 0xffu)) : et;
+    const rtn_u32 l4 = l3 + (inner == 0x86DDu ? 40u : ((vihl & 0xfu) << 2));
+    const bool is_ip = inner == 0x0800u || inner == 0x86DDu;
+    const bool need_hi = valid && is_ip && dl > 64u && l4 + 20u > 64u;
+    if (need_hi) {
+      if (a.stride >= 128u) {
+        const uint4* slot = reinterpret_cast<const uint4*>(a.slab + (rtn_u64)i * a.stride);
+#pragma unroll
+        for (int k = 4; k < 8; ++k) {
+          const uint4 x = slot[k];
+          w[4 * k + 0] = x.x; w[4 * k + 1] = x.y; w[4 * k + 2] = x.z; w[4 * k + 3] = x.w;
+        }
+      } else {
+        acc.status |= 1u;  // slot narrower than the headers this packet needs
+      }
+    }
+  }
+  rtn_view v;
+  rtn_parse(w, dl, v);
+  rtn_u32 act = 0;
+  rtn_u64 dm[RTN_DM_WORDS];
+#pragma unroll
+  for (int k = 0; k < RTN_DM_WORDS; ++k) dm[k] = 0ull;
+  rtn_filter(v, act, dm);
+  const bool pc = valid && (act & 1u) != 0u;
+  const bool fwd = pc && v.l4ok;
+  const rtn_u64 pcm = __ballot(pc);
+  const rtn_u64 fwdm = __ballot(fwd);
+  acc.pc += (rtn_u32)__popcll(pcm);
+  acc.fwd += (rtn_u32)__popcll(fwdm);
+#if !defined(RTN_NO_PREFETCH) && !defined(RTN_NO_DRAIN) && !defined(RTN_UNROLL2) && !defined(RTN_LDS_XPOSE)
+  // Drain point: the next group's loads (issued before this group was processed) have had the
+  // whole parse to land. Waiting here, before this group's stores, means no later wait ever has
+  // to cover a store (vmcnt counts stores on CDNA and drains in issue order).
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+  if (lane == 0u) {
+    a.pc_bm[wv] = pcm;
+    a.fwd_bm[wv] = fwdm;
+  }
+#ifndef RTN_EXP_NO_STORES
+  if (fwd) {
+    const rtn_u32 slot_i = wv * 64u + (rtn_u32)__popcll(fwdm & lane_lt);
+    const bool tcp = v.tcp;
+    const rtn_u32 thl = tcp ? ((rtn_l4_b(v, 12) & 0xf0u) >> 2) : 8u;
+    const rtn_u32 ihl4 = (rtn_l3_b(v, 0) & 0xfu) << 2;
+    const rtn_u32 iplen = v.v4 ? rtn_l3_be16(v, 2) : rtn_l3_be16(v, 4);
+    const rtn_u32 len = iplen - (v.v4 ? ihl4 + thl : thl);
+    uint4 r0, r1;
+    r0.x = i;
+    r0.y = v.v4 ? rtn_l3_be32(v, 12) : 0u;
+    r0.z = v.v4 ? rtn_l3_be32(v, 16) : 0u;
+    r0.w = rtn_l4_be16(v, 0) | (rtn_l4_be16(v, 2) << 16);
+    r1.x = tcp ? rtn_l4_be32(v, 4) : 0u;
+    r1.y = tcp ? rtn_l4_be32(v, 8) : 0u;
+    r1.z = (v.l4off + thl) | (len << 16);
+    r1.w = (tcp ? 6u : 17u) | ((tcp ? rtn_l4_b(v, 13) : 0u) << 8) | ((v.v4 ? 4u : 6u) << 16);
+#ifdef RTN_EXP_STORE_WINDOW
+    uint4* rp = reinterpret_cast<uint4*>(a.recs + (slot_i & 0xFFFFu));
+#else
+    uint4* rp = reinterpret_cast<uint4*>(a.recs + slot_i);
+#endif
+#ifdef RTN_NT_STORES
+    rtn_v4u* vp = reinterpret_cast<rtn_v4u*>(rp);
+    __builtin_nontemporal_store(rtn_v4u{r0.x, r0.y, r0.z, r0.w}, vp);
+    __builtin_nontemporal_store(rtn_v4u{r1.x, r1.y, r1.z, r1.w}, vp + 1);
+#else
+    rp[0] = r0;
+    rp[1] = r1;
+#endif
+    if (v.v6 && (a.flags & 1u)) {
+      uint4* ap = reinterpret_cast<uint4*>(a.addr6 + (rtn_u64)slot_i * 32u);
+      ap[0] = make_uint4(v.l3w[2], v.l3w[3], v.l3w[4], v.l3w[5]);
+      ap[1] = make_uint4(v.l3w[6], v.l3w[7], v.l3w[8], v.l3w[9]);
+    }
+  }
+#endif
+#if RTN_DELIVER_WORDS > 0
+  {
+    rtn_u64 any = 0;
+#pragma unroll
+    for (int k = 0; k < RTN_DELIVER_WORDS; ++k) any |= dm[k];
+    const bool d = valid && any != 0ull;
+    const rtn_u64 dlvm = __ballot(d);
+    if (lane == 0u) a.dlv_bm[wv] = dlvm;
+    acc.dlv += (rtn_u32)__popcll(dlvm);
+    if (d) {
+      const rtn_u64 slot_i = (rtn_u64)wv * 64u + (rtn_u64)__popcll(dlvm & lane_lt);
+      rtn_u64* dp = a.dlv_recs + slot_i * (1u + RTN_DELIVER_WORDS);
+      dp[0] = (rtn_u64)i;
+#pragma unroll
+      for (int k = 0; k < RTN_DELIVER_WORDS; ++k) dp[1 + k] = dm[k];
+    }
+  }
+#endif
+}
+
 extern "C" __global__ void __launch_bounds__(256) rtn_pc_kernel(rtn_args a) {
+#ifdef RTN_EXP_CEILING
+  {  // experiment only: fully coalesced read of the slab (16 B per lane), the HBM-read ceiling
+    const rtn_u64 n16 = (rtn_u64)a.n * a.stride / 16u;
+    const uint4* p = reinterpret_cast<const uint4*>(a.slab);
+    rtn_u32 x = 0;
+    for (rtn_u64 k = blockIdx.x * (rtn_u64)blockDim.x + threadIdx.x; k < n16; k += (rtn_u64)gridDim.x * blockDim.x) {
+      const uint4 v = p[k];
+      x ^= v.x + v.y + v.z + v.w;
+    }
+    if (x == 0x9E3779B9u) a.counters[3] = x;
+    return;
+  }
+#endif
   const rtn_u32 lane = threadIdx.x & 63u;
   const rtn_u32 wave_g = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const rtn_u32 nwaves = (gridDim.x * blockDim.x) >> 6;
   const rtn_u32 nw = (a.n + 63u) >> 6;
   const rtn_u64 lane_lt = (lane == 0u) ? 0ull : (~0ull >> (64u - lane));
-  rtn_u32 c_pc = 0, c_fwd = 0, c_dlv = 0, status = 0;
-  for (rtn_u32 wv = wave_g; wv < nw; wv += nwaves) {
-    const rtn_u32 i = wv * 64u + lane;
-    const bool valid = i < a.n;
-    rtn_u32 w[32];
-#pragma unroll
-    for (int k = 0; k < 32; ++k) w[k] = 0u;
-    rtn_u32 dl = 0;
-    const uint4* slot = reinterpret_cast<const uint4*>(a.slab + (rtn_u64)i * a.stride);
-    if (valid) {
-      dl = a.dlen[i];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const uint4 x = slot[k];
-        w[4 * k + 0] = x.x; w[4 * k + 1] = x.y; w[4 * k + 2] = x.z; w[4 * k + 3] = x.w;
-      }
+  rtn_acc acc = {0u, 0u, 0u, 0u};
+#if defined(RTN_LDS_XPOSE)
+  __shared__ __attribute__((aligned(16))) rtn_u32 xtile[4][64 * RTN_XPITCH];
+  rtn_u32* tile = xtile[threadIdx.x >> 6];
+#if defined(RTN_UNROLL2)
+  for (rtn_u32 wv = wave_g; wv < nw; wv += 2u * nwaves) {
+    uint4 q0[4], q1[4];
+    rtn_u32 dl0, dl1 = 0, lo[16];
+    const rtn_u32 w1 = wv + nwaves;
+    rtn_load_raw(a, wv, lane, q0, dl0);
+    if (w1 < nw) rtn_load_raw(a, w1, lane, q1, dl1);
+    rtn_xpose(tile, lane, q0, lo);
+    rtn_group(a, wv, lane, lane_lt, lo, dl0, acc);
+    if (w1 < nw) {
+      rtn_xpose(tile, lane, q1, lo);
+      rtn_group(a, w1, lane, lane_lt, lo, dl1, acc);
     }
-    // Second 64 B only where a header can reach past byte 64 (IPv6, IPv4 options, VLAN+options).
-    {
-      const rtn_u32 et = ((w[3] & 0xffu) << 8) | ((w[3] >> 8) & 0xffu);
-      const rtn_u32 l3 = et == 0x8100u ? 18u : 14u;
-      const rtn_u32 vihl = l3 == 18u ? (w[4] >> 16) & 0xffu : (w[3] >> 16) & 0xffu;
-      const rtn_u32 inner = et == 0x8100u ? (((w[4] & 0xffu) << 8) | ((w[4] >> 8) & 0xffu)) : et;
-      const rtn_u32 l4 = l3 + (inner == 0x86DDu ? 40u : ((vihl & 0xfu) << 2));
-      const bool is_ip = inner == 0x0800u || inner == 0x86DDu;
-      const bool need_hi = valid && is_ip && dl > 64u && l4 + 20u > 64u;
-      if (need_hi) {
-        if (a.stride >= 128u) {
-#pragma unroll
-          for (int k = 4; k < 8; ++k) {
-            const uint4 x = slot[k];
-            w[4 * k + 0] = x.x; w[4 * k + 1] = x.y; w[4 * k + 2] = x.z; w[4 * k + 3] = x.w;
-          }
-        } else {
-          status |= 1u;  // slot narrower than the headers this packet needs
-        }
-      }
-    }
-    rtn_view v;
-    rtn_parse(w, dl, v);
-    rtn_u32 act = 0;
-    rtn_u64 dm[RTN_DM_WORDS];
-#pragma unroll
-    for (int k = 0; k < RTN_DM_WORDS; ++k) dm[k] = 0ull;
-    rtn_filter(v, act, dm);
-    const bool pc = valid && (act & 1u) != 0u;
-    const bool fwd = pc && v.l4ok;
-    const rtn_u64 pcm = __ballot(pc);
-    const rtn_u64 fwdm = __ballot(fwd);
-    if (lane == 0u) {
-      a.pc_bm[wv] = pcm;
-      a.fwd_bm[wv] = fwdm;
-    }
-    c_pc += (rtn_u32)__popcll(pcm);
-    c_fwd += (rtn_u32)__popcll(fwdm);
-    if (fwd) {
-      const rtn_u32 slot_i = wv * 64u + (rtn_u32)__popcll(fwdm & lane_lt);
-      const bool tcp = v.tcp;
-      const rtn_u32 thl = tcp ? ((rtn_l4_b(v, 12) & 0xf0u) >> 2) : 8u;
-      const rtn_u32 ihl4 = (rtn_l3_b(v, 0) & 0xfu) << 2;
-      const rtn_u32 iplen = v.v4 ? rtn_l3_be16(v, 2) : rtn_l3_be16(v, 4);
-      const rtn_u32 len = iplen - (v.v4 ? ihl4 + thl : thl);
-      uint4 r0, r1;
-      r0.x = i;
-      r0.y = v.v4 ? rtn_l3_be32(v, 12) : 0u;
-      r0.z = v.v4 ? rtn_l3_be32(v, 16) : 0u;
-      r0.w = rtn_l4_be16(v, 0) | (rtn_l4_be16(v, 2) << 16);
-      r1.x = tcp ? rtn_l4_be32(v, 4) : 0u;
-      r1.y = tcp ? rtn_l4_be32(v, 8) : 0u;
-      r1.z = (v.l4off + thl) | (len << 16);
-      r1.w = (tcp ? 6u : 17u) | ((tcp ? rtn_l4_b(v, 13) : 0u) << 8) | ((v.v4 ? 4u : 6u) << 16);
-      uint4* rp = reinterpret_cast<uint4*>(a.recs + slot_i);
-      rp[0] = r0;
-      rp[1] = r1;
-      if (v.v6 && (a.flags & 1u)) {
-        uint4* ap = reinterpret_cast<uint4*>(a.addr6 + (rtn_u64)slot_i * 32u);
-        ap[0] = make_uint4(v.l3w[2], v.l3w[3], v.l3w[4], v.l3w[5]);
-        ap[1] = make_uint4(v.l3w[6], v.l3w[7], v.l3w[8], v.l3w[9]);
-      }
-    }
-#if RTN_DELIVER_WORDS > 0
-    {
-      rtn_u64 any = 0;
-#pragma unroll
-      for (int k = 0; k < RTN_DELIVER_WORDS; ++k) any |= dm[k];
-      const bool d = valid && any != 0ull;
-      const rtn_u64 dlvm = __ballot(d);
-      if (lane == 0u) a.dlv_bm[wv] = dlvm;
-      c_dlv += (rtn_u32)__popcll(dlvm);
-      if (d) {
-        const rtn_u64 slot_i = (rtn_u64)wv * 64u + (rtn_u64)__popcll(dlvm & lane_lt);
-        rtn_u64* dp = a.dlv_recs + slot_i * (1u + RTN_DELIVER_WORDS);
-        dp[0] = (rtn_u64)i;
-#pragma unroll
-        for (int k = 0; k < RTN_DELIVER_WORDS; ++k) dp[1 + k] = dm[k];
-      }
-    }
-#endif
   }
+#else
+  uint4 q[4];
+  rtn_u32 dl = 0;
+  if (wave_g < nw) rtn_load_raw(a, wave_g, lane, q, dl);
+  for (rtn_u32 wv = wave_g; wv < nw; wv += nwaves) {
+    rtn_u32 lo[16];
+    rtn_xpose(tile, lane, q, lo);
+    const rtn_u32 cdl = dl;
+    const rtn_u32 nx = wv + nwaves;
+    if (nx < nw) rtn_load_raw(a, nx, lane, q, dl);
+    rtn_group(a, wv, lane, lane_lt, lo, cdl, acc);
+  }
+#endif
+#elif defined(RTN_UNROLL2)
+  // Two groups per iteration: both groups' loads are in flight before either is processed.
+  for (rtn_u32 wv = wave_g; wv < nw; wv += 2u * nwaves) {
+    rtn_u32 lo0[16], lo1[16], dl0, dl1 = 0;
+    const rtn_u32 w1 = wv + nwaves;
+    rtn_load_lo(a, wv * 64u + lane, wv * 64u + lane < a.n, lo0, dl0);
+    if (w1 < nw) rtn_load_lo(a, w1 * 64u + lane, w1 * 64u + lane < a.n, lo1, dl1);
+    rtn_group(a, wv, lane, lane_lt, lo0, dl0, acc);
+    if (w1 < nw) rtn_group(a, w1, lane, lane_lt, lo1, dl1, acc);
+  }
+#elif !defined(RTN_NO_PREFETCH)
+  // Software pipeline: the next group's first 64 B are in flight while this group is processed.
+  rtn_u32 lo[16], dl;
+  if (wave_g < nw) rtn_load_lo(a, wave_g * 64u + lane, wave_g * 64u + lane < a.n, lo, dl);
+  for (rtn_u32 wv = wave_g; wv < nw; wv += nwaves) {
+    rtn_u32 nlo[16], ndl = 0;
+    const rtn_u32 nx = wv + nwaves;
+    if (nx < nw) rtn_load_lo(a, nx * 64u + lane, nx * 64u + lane < a.n, nlo, ndl);
+    rtn_group(a, wv, lane, lane_lt, lo, dl, acc);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) lo[k] = nlo[k];
+    dl = ndl;
+  }
+#else
+  for (rtn_u32 wv = wave_g; wv < nw; wv += nwaves) {
+    rtn_u32 lo[16], dl;
+    rtn_load_lo(a, wv * 64u + lane, wv * 64u + lane < a.n, lo, dl);
+    rtn_group(a, wv, lane, lane_lt, lo, dl, acc);
+  }
+#endif
   // one set of atomics per wave
+  const rtn_u64 st = __ballot(acc.status != 0u);
+  if (lane == 0u && st) atomicOr(&a.counters[3], 1u);
   if (!(a.flags & 2u)) return;
   if (lane == 0u) {
-    if (c_pc) atomicAdd(&a.counters[0], c_pc);
-    if (c_fwd) atomicAdd(&a.counters[1], c_fwd);
-    if (c_dlv) atomicAdd(&a.counters[2], c_dlv);
+    if (acc.pc) atomicAdd(&a.counters[0], acc.pc);
+    if (acc.fwd) atomicAdd(&a.counters[1], acc.fwd);
+    if (acc.dlv) atomicAdd(&a.counters[2], acc.dlv);
   }
-  const rtn_u64 st = __ballot(status != 0u);
-  if (lane == 0u && st) atomicOr(&a.counters[3], 1u);
 }

@@ -40,6 +40,18 @@ std::string build_source(const rtn::PacketProgram& prog) {
   const std::string marker = "//@@RTN_FILTER@@";
   size_t at = tpl.find(marker);
   std::string head = "#define RTN_DELIVER_WORDS " + std::to_string(prog.deliver_words()) + "\n";
+  // Kernel variants for experiments (e.g. "RTN_NO_PREFETCH"); never set in production runs.
+  if (const char* d = getenv("RTN_KERNEL_DEFINES")) {
+    std::string all = d, tok;
+    for (size_t k = 0; k <= all.size(); ++k) {
+      if (k == all.size() || all[k] == ',') {
+        if (!tok.empty()) head += "#define " + tok + "\n";
+        tok.clear();
+      } else if (all[k] != ' ') {
+        tok += all[k] == '=' ? ' ' : all[k];
+      }
+    }
+  }
   return head + tpl.substr(0, at) + prog.hip_body + tpl.substr(at + marker.size());
 }
 
