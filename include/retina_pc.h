@@ -43,17 +43,25 @@ extern "C" {
 typedef struct rtn_program rtn_program_t; /* compiled subscription set (host only)        */
 typedef struct rtn_pc rtn_pc_t;           /* program loaded on one device, ready to run  */
 
-/* Compacted L4Context of a forwarded packet (PacketContinue && L4Context::new Ok). 32 bytes. */
+/* Compacted L4Context of a forwarded packet (PacketContinue && L4Context::new Ok), 24 bytes:
+ * every field of conntrack/pdu.rs:66-84. The frame it belongs to is implied by the record's
+ * position (see rtn_pc_out_t). */
 typedef struct rtn_l4ctx {
-  uint32_t pkt_idx;     /* index of the packet within the batch                          */
-  uint32_t src_ip4;     /* u32::from(Ipv4Addr) (host order); 0 for IPv6, see addr6 array  */
+  uint32_t src_ip4; /* u32::from(Ipv4Addr) (host order); 0 for IPv6, see addr6 array     */
   uint32_t dst_ip4;
-  uint32_t ports;       /* src_port | dst_port << 16                                      */
-  uint32_t seq_no;      /* TCP only (0 for UDP)                                           */
-  uint32_t ack_no;      /* TCP only                                                        */
-  uint32_t off_len;     /* L4Context.offset | L4Context.length << 16                     */
-  uint32_t proto_flags; /* proto (6/17) | tcp flags << 8 | ip version (4/6) << 16          */
+  uint32_t ports;   /* src_port | dst_port << 16                                         */
+  uint32_t seq_no;  /* TCP only (0 for UDP)                                              */
+  uint32_t ack_no;  /* TCP only                                                          */
+  uint32_t meta;    /* RTN_L4_* accessors below: offset, proto, ip version, flags, length */
 } rtn_l4ctx_t;
+
+/* L4Context.offset is always 2 mod 4 (14/18-byte L2 + 4*IHL or 40 + 4*doff or 8), so it is
+ * stored as offset >> 2 in 6 bits. */
+#define RTN_L4_OFFSET(m) ((((m) & 0x3Fu) << 2) | 2u)            /* L4Context.offset           */
+#define RTN_L4_PROTO(m) (((m) & 0x40u) ? 17u : 6u)                 /* L4Context.proto            */
+#define RTN_L4_IPV6(m) (((m) >> 7) & 1u)                           /* src/dst are IPv6 (addr6)   */
+#define RTN_L4_FLAGS(m) (((m) >> 8) & 0xFFu)                       /* L4Context.flags (TCP)      */
+#define RTN_L4_LENGTH(m) ((m) >> 16)                               /* L4Context.length           */
 
 /* A batch of frames laid out for coalesced HBM reads: slot i (stride bytes, a multiple of 64)
  * holds the first min(data_len[i], stride) bytes of frame i. stride >= 128 is always valid;
@@ -66,15 +74,18 @@ typedef struct rtn_batch {
   uint32_t core_id;         /* the calling lcore (passed to CoreId callbacks by the host) */
 } rtn_batch_t;
 
-/* Outputs, segmented per 64-frame group g = i / 64: entry j of group g is at [g * 64 + j];
- * group g holds popcount(bitmap[g]) entries, in frame order. */
+/* Record arrays are dense per chunk of RTN_CHUNK_FRAMES frames, in frame order: the k-th
+ * forwarded frame of chunk c = i / RTN_CHUNK_FRAMES has its L4Context at l4[c * RTN_CHUNK_FRAMES + k]
+ * (k = popcount of fwd_bitmap over the chunk's frames before it); likewise addr6 (same index)
+ * and dlv_records (ranked by dlv_bitmap). Bitmaps hold bit i % 64 of word i / 64 for frame i. */
+#define RTN_CHUNK_FRAMES 1024u
 typedef struct rtn_pc_out {
   uint64_t* pc_bitmap;   /* [ceil(n/64)]  Actions.data contains PacketContinue               */
   uint64_t* fwd_bitmap;  /* [ceil(n/64)]  ... and L4Context::new succeeded (goes to conntrack) */
-  rtn_l4ctx_t* l4;       /* [ceil(n/64)*64]                                                   */
-  uint8_t* addr6;        /* optional [ceil(n/64)*64][32]: IPv6 src|dst bytes of IPv6 records  */
+  rtn_l4ctx_t* l4;       /* [ceil(n/1024)*1024] (rtn_out_l4_bytes); unused slots undefined    */
+  uint8_t* addr6;        /* optional [ceil(n/1024)*1024][32]: IPv6 src|dst bytes of IPv6 records */
   uint64_t* dlv_bitmap;  /* [ceil(n/64)] frames with >= 1 packet-level callback (if any)     */
-  uint64_t* dlv_records; /* [ceil(n/64)*64][1 + deliver_words]: frame index, statement mask  */
+  uint64_t* dlv_records; /* [ceil(n/1024)*1024][1 + deliver_words]: frame index, statement mask */
   uint32_t* counters;    /* optional [4]: pc, fwd, dlv totals, status bits; zeroed per run
                           (NULL: no totals, no memset -- the run is a single kernel launch) */
 } rtn_pc_out_t;

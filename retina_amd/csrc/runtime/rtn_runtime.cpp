@@ -131,7 +131,8 @@ struct rtn_pc {
   const rtn_program* program = nullptr;
   int device = 0;
   hipModule_t module = nullptr;
-  hipFunction_t fn = nullptr;
+  hipFunction_t fn = nullptr;      // rtn_pc_kernel: any stride (multiple of 64)
+  hipFunction_t fn_s64 = nullptr;  // rtn_pc_kernel_s64: 64-byte slots
   uint32_t blocks = 0;
   uint32_t* scratch_counters = nullptr;  // used when the caller passes no counters
 };
@@ -247,6 +248,8 @@ int32_t rtn_pc_create_from_program(rtn_program_t* p, int device, rtn_pc_t** out)
   if (e != hipSuccess) return fail(RTN_EDEVICE, std::string("hipModuleLoadData: ") + hipGetErrorString(e));
   e = hipModuleGetFunction(&pc->fn, pc->module, "rtn_pc_kernel");
   if (e != hipSuccess) return fail(RTN_EDEVICE, std::string("hipModuleGetFunction: ") + hipGetErrorString(e));
+  e = hipModuleGetFunction(&pc->fn_s64, pc->module, "rtn_pc_kernel_s64");
+  if (e != hipSuccess) return fail(RTN_EDEVICE, std::string("hipModuleGetFunction: ") + hipGetErrorString(e));
   e = hipMalloc(&pc->scratch_counters, 16);
   if (e != hipSuccess) return fail(RTN_EDEVICE, std::string("hipMalloc: ") + hipGetErrorString(e));
   if (const char* g = getenv("RTN_GRID")) pc->blocks = (uint32_t)strtoul(g, nullptr, 10);
@@ -302,13 +305,14 @@ int32_t rtn_pc_run(rtn_pc_t* pc, const rtn_batch_t* in, rtn_pc_out_t* out, void*
   a.dlv_bm = out->dlv_bitmap;
   a.dlv_recs = out->dlv_records;
   a.counters = out->counters ? out->counters : pc->scratch_counters;
-  const uint32_t groups = (in->n + 63u) / 64u;
+  const uint32_t chunks = (in->n + RTN_CHUNK_FRAMES - 1u) / RTN_CHUNK_FRAMES;
   uint32_t blocks = pc->blocks ? pc->blocks : 2048u;
-  const uint32_t need = (groups + 3u) / 4u;
+  const uint32_t need = (chunks + 3u) / 4u;  // one wave per chunk at most
   if (blocks > need) blocks = need;
   if (blocks == 0) blocks = 1;
   void* params[] = {&a};
-  e = hipModuleLaunchKernel(pc->fn, blocks, 1, 1, 256, 1, 1, 0, s, params, nullptr);
+  hipFunction_t fn = in->stride == 64 ? pc->fn_s64 : pc->fn;
+  e = hipModuleLaunchKernel(fn, blocks, 1, 1, 256, 1, 1, 0, s, params, nullptr);
   if (e != hipSuccess) return fail(RTN_EDEVICE, std::string("hipModuleLaunchKernel: ") + hipGetErrorString(e));
   return RTN_OK;
 }
@@ -323,10 +327,12 @@ int32_t rtn_pc_destroy(rtn_pc_t* pc) {
 }
 
 size_t rtn_out_bitmap_bytes(uint32_t n) { return (size_t)((n + 63u) / 64u) * 8u; }
-size_t rtn_out_l4_bytes(uint32_t n) { return (size_t)((n + 63u) / 64u) * 64u * sizeof(rtn_l4ctx_t); }
-size_t rtn_out_addr6_bytes(uint32_t n) { return (size_t)((n + 63u) / 64u) * 64u * 32u; }
+static size_t chunked(uint32_t n) { return (size_t)((n + RTN_CHUNK_FRAMES - 1u) / RTN_CHUNK_FRAMES) * RTN_CHUNK_FRAMES; }
+static_assert(sizeof(rtn_l4ctx_t) == 24, "rtn_l4ctx_t is 24 bytes");
+size_t rtn_out_l4_bytes(uint32_t n) { return chunked(n) * sizeof(rtn_l4ctx_t); }
+size_t rtn_out_addr6_bytes(uint32_t n) { return chunked(n) * 32u; }
 size_t rtn_out_dlv_bytes(uint32_t n, uint32_t deliver_words) {
-  return (size_t)((n + 63u) / 64u) * 64u * (1u + deliver_words) * 8u;
+  return chunked(n) * (1u + deliver_words) * 8u;
 }
 
 }  // extern "C"

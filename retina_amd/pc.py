@@ -94,8 +94,31 @@ def _text(fn, h) -> str:
     return buf.value.decode()
 
 
-L4_DTYPE = np.dtype([("pkt_idx", "<u4"), ("src_ip4", "<u4"), ("dst_ip4", "<u4"), ("ports", "<u4"),
-                     ("seq_no", "<u4"), ("ack_no", "<u4"), ("off_len", "<u4"), ("proto_flags", "<u4")])
+# rtn_l4ctx_t (include/retina_pc.h), 24 bytes
+L4_DTYPE = np.dtype([("src_ip4", "<u4"), ("dst_ip4", "<u4"), ("ports", "<u4"), ("seq_no", "<u4"),
+                     ("ack_no", "<u4"), ("meta", "<u4")])
+# what PCOutputs.decode() returns per forwarded frame: the record's fields unpacked, plus the
+# frame index its position implies
+L4_DECODED = np.dtype([("pkt_idx", "<u8"), ("src_ip4", "<u4"), ("dst_ip4", "<u4"), ("sport", "<u4"),
+                       ("dport", "<u4"), ("seq_no", "<u4"), ("ack_no", "<u4"), ("offset", "<u4"),
+                       ("length", "<u4"), ("proto", "<u4"), ("flags", "<u4"), ("ver", "<u4")])
+
+
+def decode_l4(raw: np.ndarray, frames: np.ndarray) -> np.ndarray:
+    """Unpack rtn_l4ctx_t records (the RTN_L4_* accessors of retina_pc.h)."""
+    out = np.zeros(len(raw), L4_DECODED)
+    out["pkt_idx"] = frames
+    for f in ("src_ip4", "dst_ip4", "seq_no", "ack_no"):
+        out[f] = raw[f]
+    out["sport"] = raw["ports"] & 0xFFFF
+    out["dport"] = raw["ports"] >> 16
+    m = raw["meta"]
+    out["offset"] = ((m & 0x3F) << 2) | 2
+    out["proto"] = np.where(m & 0x40, 17, 6)
+    out["ver"] = np.where(m & 0x80, 6, 4)
+    out["flags"] = (m >> 8) & 0xFF
+    out["length"] = m >> 16
+    return out
 
 
 class Program:
@@ -180,7 +203,7 @@ class PCOutputs:
         fwd = np.unpackbits(fwd_bm.view(np.uint8), bitorder="little")[:n].astype(bool)
         recs_all = self.l4.cpu().numpy().view(L4_DTYPE)
         idx = _segment_index(fwd_bm)
-        recs = recs_all[idx]
+        recs = decode_l4(recs_all[idx], np.nonzero(fwd)[0])
         out = {"pc": pc, "fwd": fwd, "l4": recs}
         if self.addr6 is not None:
             a6 = self.addr6.cpu().numpy().view(np.uint8).reshape(-1, 32)
@@ -193,14 +216,20 @@ class PCOutputs:
         return out
 
 
+CHUNK_FRAMES = 1024  # RTN_CHUNK_FRAMES (include/retina_pc.h)
+
+
 def _segment_index(bm: np.ndarray) -> np.ndarray:
-    counts = np.unpackbits(bm.view(np.uint8), bitorder="little").reshape(-1, 64).sum(1).astype(np.int64)
-    total = int(counts.sum())
-    if total == 0:
+    """Record-array index of every set bit of `bm`, in frame order: records are dense per chunk
+    of CHUNK_FRAMES frames, starting at chunk * CHUNK_FRAMES."""
+    bits = np.unpackbits(bm.view(np.uint8), bitorder="little").astype(np.int64)
+    frames = np.nonzero(bits)[0]
+    if frames.size == 0:
         return np.zeros(0, np.int64)
-    starts = np.repeat(np.arange(len(bm), dtype=np.int64) * 64, counts)
-    first = np.repeat(np.cumsum(counts) - counts, counts)
-    return starts + (np.arange(total, dtype=np.int64) - first)
+    chunk = frames // CHUNK_FRAMES
+    # rank within the chunk = number of set bits of the same chunk before it
+    first = np.searchsorted(chunk, chunk, side="left")
+    return chunk * CHUNK_FRAMES + (np.arange(frames.size, dtype=np.int64) - first)
 
 
 class PacketContinue:

@@ -56,14 +56,9 @@ def gpu_run(spec: str, slab: np.ndarray, stride: int, dlen: np.ndarray, device: 
     cnt = out.counters_host()
     l4 = d["l4"]
     rec = np.zeros(len(l4), REC)
+    for f in ("ver", "proto", "flags", "sport", "dport", "offset", "length"):
+        rec[f] = l4[f]
     rec["idx"] = l4["pkt_idx"]
-    rec["ver"] = (l4["proto_flags"] >> 16) & 0xFF
-    rec["proto"] = l4["proto_flags"] & 0xFF
-    rec["flags"] = (l4["proto_flags"] >> 8) & 0xFF
-    rec["sport"] = l4["ports"] & 0xFFFF
-    rec["dport"] = l4["ports"] >> 16
-    rec["offset"] = l4["off_len"] & 0xFFFF
-    rec["length"] = l4["off_len"] >> 16
     rec["seq"] = l4["seq_no"]
     rec["ack"] = l4["ack_no"]
     v4 = rec["ver"] == 4

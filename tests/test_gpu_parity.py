@@ -106,8 +106,8 @@ def test_full_size_cfg2_properties(gpu):
     assert np.array_equal(d["fwd"], exp)
     l4 = d["l4"]
     assert np.array_equal(l4["pkt_idx"], np.nonzero(exp)[0])
-    assert np.all(l4["off_len"] == (54 | (10 << 16)))
-    assert np.all(l4["ports"] >> 16 == 80)
+    assert np.all(l4["offset"] == 54) and np.all(l4["length"] == 10)
+    assert np.all(l4["dport"] == 80) and np.all(l4["proto"] == 6) and np.all(l4["ver"] == 4)
     c = out.counters_host()
     assert c[0] == exp.sum() and c[1] == exp.sum() and c[3] == 0
     lo = 3 << 22
