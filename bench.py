@@ -183,9 +183,9 @@ def main() -> None:
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    from retina_amd import dist as rdist
+
+    rank, world, local = rdist.env_rank()
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -197,7 +197,8 @@ def main() -> None:
     cfg = args.config
     _, stride, n_default, desc = CONFIGS[cfg]
     n = args.frames or n_default
-    slab, dlen = gen_frames(cfg, n, start=rank * n)
+    sh = rdist.shard(n, rank, world)  # weak scaling: a disjoint shard of the frame stream per rank
+    slab, dlen = gen_frames(cfg, sh.count, start=sh.start)
     alg_bytes = synth.alg_read_bytes(slab, dlen, stride)
     d_slab = torch.from_numpy(slab).to(dev)
     d_dlen = torch.from_numpy(dlen.view(np.int16)).to(dev)
@@ -232,17 +233,13 @@ def main() -> None:
     ctx.run(d_slab, stride, d_dlen, n, cnt_out, stream=stream)
     torch.cuda.synchronize(dev)
     counters = cnt_out.counters.view(torch.int32)[:3].to(torch.int64)
-    stats = torch.tensor([wall, kern_ms, float(alg_bytes)], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(counters, op=dist.ReduceOp.SUM)
-        mx = stats.clone()
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        wall, kern_ms = float(mx[0]), float(mx[1])
+    stats = torch.tensor([wall, kern_ms], dtype=torch.float64, device=dev)
+    rdist.reduce_totals(counters, stats)  # sum / max over ranks (RCCL), outside the timed region
+    wall, kern_ms = float(stats[0]), float(stats[1])
     counters = counters.cpu().tolist()
 
     if rank == 0:
-        total = n * world * args.steps
-        value = total / wall / 1e6
+        value = rdist.aggregate_mpps(n, world, args.steps, wall)
         achieved = alg_bytes / (kern_ms / 1e3) / 1e9
         cpu = None
         if not args.no_cpu and world == 1:

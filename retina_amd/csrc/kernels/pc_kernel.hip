@@ -104,6 +104,14 @@ __device__ __forceinline__ rtn_u32 rtn_mask(bool b) {
 }
 __device__ __forceinline__ rtn_u32 rtn_sel(rtn_u32 m, rtn_u32 a, rtn_u32 b) { return (a & m) | (b & ~m); }
 
+// LDS visibility between lanes of one wave (LDS executes a wave's instructions in order; this
+// keeps the compiler from reordering across the hand-off).
+__device__ __forceinline__ void rtn_wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 template <int NW>
 __device__ __forceinline__ rtn_u32 rtn_w(const rtn_u32 (&w)[NW], int k) { return k < NW ? w[k] : 0u; }
 
@@ -226,6 +234,36 @@ __device__ __forceinline__ void rtn_load_lo(const rtn_args& a, rtn_u32 i, rtn_u3
   dl = valid ? d : 0u;
 }
 
+#ifdef RTN_XPOSE
+// 64-byte slots, coalesced: the group's 4 KB arrive as four full-width 16-B-per-lane loads
+// (lane l of load k holds quarter l%4 of slot 16k + l/4) and an LDS tile (80-B pitch, conflict-
+// free ds_read_b128) turns them back into one slot per lane.
+#define RTN_XPITCH 20u
+__device__ __forceinline__ void rtn_load_group(const rtn_args& a, rtn_u32 g, rtn_u32 lane, rtn_v4u (&q)[4], rtn_u32& dl) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const rtn_u32 slot = g * 64u + 16u * k + (lane >> 2);
+    const rtn_u32 sc = slot < a.n ? slot : a.n - 1u;
+    q[k] = RTN_LD(reinterpret_cast<const rtn_v4u*>(a.slab + (rtn_u64)sc * 64u) + (lane & 3u));
+  }
+  const rtn_u32 i = g * 64u + lane;
+  const rtn_u32 d = a.dlen[i < a.n ? i : a.n - 1u];
+  dl = i < a.n ? d : 0u;
+}
+__device__ __forceinline__ void rtn_xpose(rtn_u32* tile, rtn_u32 lane, const rtn_v4u (&q)[4], rtn_u32 (&w)[16]) {
+  rtn_wave_sync();
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    *reinterpret_cast<rtn_v4u*>(tile + (16u * k + (lane >> 2)) * RTN_XPITCH + (lane & 3u) * 4u) = q[k];
+  rtn_wave_sync();
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const rtn_v4u x = *reinterpret_cast<const rtn_v4u*>(tile + lane * RTN_XPITCH + 4u * j);
+    w[4 * j + 0] = x.x; w[4 * j + 1] = x.y; w[4 * j + 2] = x.z; w[4 * j + 3] = x.w;
+  }
+}
+#endif
+
 // Second 64 B of a slot, only for lanes whose headers can reach past byte 64 (IPv6, IPv4
 // options, VLAN + options) and only when the slot holds them.
 __device__ __forceinline__ bool rtn_need_hi(const rtn_u32 (&w)[16], rtn_u32 dl) {
@@ -248,18 +286,16 @@ struct rtn_chunk {
   rtn_u64 my_pc, my_fwd, my_dlv;  // lane k holds group k's bitmap words until the chunk ends
 };
 
-// LDS visibility between lanes of one wave (LDS executes a wave's instructions in order; this
-// keeps the compiler from reordering across the hand-off).
-__device__ __forceinline__ void rtn_wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 // Records leave through a per-wave LDS ring of 256 records (6 KB) as whole 128-record blocks:
 // three full-width 16-B-per-lane stores per 3 KB, every line written whole.
+#ifdef RTN_XPOSE
+#define RTN_RING 128u   // leaves LDS room for the transpose tile
+#define RTN_FLUSH 64u
+#else
 #define RTN_RING 256u
 #define RTN_FLUSH 128u
+#endif
 
 __device__ __forceinline__ void rtn_flush(const rtn_args& a, const rtn_u64* ring, const rtn_chunk& ch, rtn_u32 lane,
                                           rtn_u32 nrecs) {
@@ -325,7 +361,7 @@ __device__ __forceinline__ void rtn_group(const rtn_args& a, rtn_u32 g, rtn_u32 
     }
   }
   ch.nrec += nfwd;
-  if (ch.nrec - ch.nflushed >= RTN_FLUSH) {  // pending < 128 + 64: at most one block per group
+  if (ch.nrec - ch.nflushed >= RTN_FLUSH) {  // pending < RTN_FLUSH + 64 <= RTN_RING: one block per group
     rtn_wave_sync();
     rtn_flush(a, ring, ch, lane, RTN_FLUSH);
     ch.nflushed += RTN_FLUSH;
@@ -367,22 +403,41 @@ __device__ __forceinline__ void rtn_run(const rtn_args& a) {
   rtn_acc acc = {0u, 0u, 0u, 0u};
   __shared__ __attribute__((aligned(16))) rtn_u64 rtn_ring[4][RTN_RING * 3u];
   rtn_u64* ring = rtn_ring[threadIdx.x >> 6];
+#ifdef RTN_XPOSE
+  __shared__ __attribute__((aligned(16))) rtn_u32 rtn_tile[4][64 * RTN_XPITCH];
+  rtn_u32* tile = rtn_tile[threadIdx.x >> 6];
+#endif
   for (rtn_u32 c = wave_g; c < nchunks; c += nwaves) {
     const rtn_u32 gb = c * RTN_CHUNK_GROUPS;
     const rtn_u32 ge = gb + RTN_CHUNK_GROUPS < nw ? gb + RTN_CHUNK_GROUPS : nw;
     rtn_chunk ch = {(rtn_u64)c * (64u * RTN_CHUNK_GROUPS), 0u, 0u, 0u, 0ull, 0ull, 0ull};
     for (rtn_u32 g0 = gb; g0 < ge; g0 += RTN_UNROLL) {
       rtn_u32 lo[RTN_UNROLL][16], dl[RTN_UNROLL];
+#ifdef RTN_XPOSE
+      rtn_v4u q[RTN_UNROLL][4];
+      if (S64) {
 #pragma unroll
-      for (int u = 0; u < RTN_UNROLL; ++u) {
-        const rtn_u32 g = g0 + u;
-        if (u == 0 || g < ge) rtn_load_lo(a, g * 64u + lane, lo[u], dl[u]);
+        for (int u = 0; u < RTN_UNROLL; ++u) {
+          const rtn_u32 g = g0 + u;
+          if (u == 0 || g < ge) rtn_load_group(a, g, lane, q[u], dl[u]);
+        }
+      } else
+#endif
+      {
+#pragma unroll
+        for (int u = 0; u < RTN_UNROLL; ++u) {
+          const rtn_u32 g = g0 + u;
+          if (u == 0 || g < ge) rtn_load_lo(a, g * 64u + lane, lo[u], dl[u]);
+        }
       }
 #pragma unroll
       for (int u = 0; u < RTN_UNROLL; ++u) {
         const rtn_u32 g = g0 + u;
         if (u > 0 && g >= ge) break;
         if (S64) {
+#ifdef RTN_XPOSE
+          rtn_xpose(tile, lane, q[u], lo[u]);
+#endif
           rtn_group<16>(a, g, g - gb, lane, lane_lt, lo[u], dl[u], ring, ch, acc);
         } else {
           rtn_u32 w[32];
