@@ -1,0 +1,50 @@
+/*
+ * retina_ingest.h — offline ingest for the MI355X packet stage: a capture file -> slot slab.
+ *
+ * Replaces, for the batched path, what the reference's offline runtime does before the packet
+ * filter (core/src/runtime/offline.rs:64-82):
+ *   - Capture::from_file(pcap) (pcap crate; libpcap and pcapng files)         offline.rs:64-65
+ *   - skip a frame whose original (wire) length exceeds the configured mtu    offline.rs:68-70
+ *   - Mbuf::from_bytes(frame.data): mbuf data = the captured bytes, data_len = their count
+ *                                                            core/src/memory/mbuf.rs:56-76
+ * Frames are packed, in file order, into the slot layout rtn_pc_run reads (retina_pc.h): slot i
+ * (stride bytes) receives the first min(data_len[i], stride) captured bytes; bytes past that
+ * are left as they were (the kernel never reads past data_len). Same error conventions as
+ * retina_pc.h (0 or a negative RTN_* code; rtn_last_error()).
+ */
+#ifndef RETINA_INGEST_H
+#define RETINA_INGEST_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct rtn_pcap rtn_pcap_t;
+
+typedef struct rtn_pcap_stats {
+  uint64_t frames;       /* frames read from the file                                   */
+  uint64_t skipped_mtu;  /* ... of which skipped: original length > mtu (offline.rs:68) */
+  uint64_t packed;       /* ... of which handed to the filter                          */
+  uint64_t bytes;        /* captured bytes of the packed frames (offline.rs nb_bytes)  */
+} rtn_pcap_stats_t;
+
+/* Open a libpcap (either byte order, us or ns timestamps) or pcapng capture. */
+int32_t rtn_pcap_open(const char* path, uint32_t mtu, rtn_pcap_t** out);
+/* Pack up to `cap` frames into slab/data_len (host memory, e.g. pinned); *n = frames packed,
+ * 0 at end of file. A captured frame longer than 65535 bytes (beyond Mbuf::data_len's u16)
+ * fails with RTN_ERANGE. */
+int32_t rtn_pcap_next_batch(rtn_pcap_t* p, uint8_t* slab, uint64_t stride, uint16_t* data_len, uint32_t cap,
+                            uint32_t* n);
+int32_t rtn_pcap_stats(const rtn_pcap_t* p, rtn_pcap_stats_t* st);
+/* Start again from the first frame (stats are kept). */
+int32_t rtn_pcap_rewind(rtn_pcap_t* p);
+void rtn_pcap_close(rtn_pcap_t* p);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RETINA_INGEST_H */

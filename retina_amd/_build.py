@@ -49,14 +49,15 @@ def build_library(force: bool = False) -> Path:
     LIB.mkdir(exist_ok=True)
     inc = _gen_kernel_inc()
     fg = [CSRC / "filtergen" / s for s in FILTERGEN_SRCS]
-    rt = CSRC / "runtime" / "rtn_runtime.cpp"
-    hdrs = list((CSRC / "filtergen").glob("*.hpp")) + [ROOT / "include" / "retina_pc.h", inc]
+    rt = [CSRC / "runtime" / "rtn_runtime.cpp", CSRC / "ingest" / "pcap_ingest.cpp"]
+    hdrs = (list((CSRC / "filtergen").glob("*.hpp")) + list((CSRC / "runtime").glob("*.hpp"))
+            + list((ROOT / "include").glob("*.h")) + [inc])
     so = LIB / SO_NAME
-    if force or _stale(so, fg + [rt] + hdrs):
+    if force or _stale(so, fg + rt + hdrs):
         cmd = [
             "g++", "-std=c++17", "-O2", "-fPIC", "-shared", "-Wall", "-Wextra", "-Wno-unused-parameter",
             "-D__HIP_PLATFORM_AMD__", f"-I{ROOT / 'include'}", f"-I{ROCM / 'include'}",
-            *map(str, fg), str(rt), "-o", str(so),
+            *map(str, fg), *map(str, rt), "-o", str(so),
             f"-L{ROCM / 'lib'}", f"-Wl,-rpath,{ROCM / 'lib'}", "-lamdhip64", "-lhiprtc",
         ]
         _run(cmd)

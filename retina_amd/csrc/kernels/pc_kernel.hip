@@ -47,6 +47,17 @@ typedef unsigned int rtn_v4u __attribute__((ext_vector_type(4)));
 #else
 #define RTN_LD(p) (*(p))
 #endif
+// 64-byte slots load coalesced + LDS transpose (RTN_XPOSE) with non-temporal loads: every line
+// is touched once, so streaming it past the caches costs nothing (per-lane loads touch each
+// line four times and must not be non-temporal).
+#ifndef RTN_NO_XPOSE
+#define RTN_XPOSE 1
+#endif
+#ifdef RTN_XPOSE_TEMPORAL
+#define RTN_LD_STREAM(p) (*(p))
+#else
+#define RTN_LD_STREAM(p) __builtin_nontemporal_load(p)
+#endif
 
 struct rtn_l4rec {       // 24 B, the compacted L4Context of a forwarded packet (rtn_l4ctx_t)
   rtn_u32 src_ip4;       // u32::from(Ipv4Addr) (0 for IPv6; addresses in addr6 side array)
@@ -244,7 +255,7 @@ __device__ __forceinline__ void rtn_load_group(const rtn_args& a, rtn_u32 g, rtn
   for (int k = 0; k < 4; ++k) {
     const rtn_u32 slot = g * 64u + 16u * k + (lane >> 2);
     const rtn_u32 sc = slot < a.n ? slot : a.n - 1u;
-    q[k] = RTN_LD(reinterpret_cast<const rtn_v4u*>(a.slab + (rtn_u64)sc * 64u) + (lane & 3u));
+    q[k] = RTN_LD_STREAM(reinterpret_cast<const rtn_v4u*>(a.slab + (rtn_u64)sc * 64u) + (lane & 3u));
   }
   const rtn_u32 i = g * 64u + lane;
   const rtn_u32 d = a.dlen[i < a.n ? i : a.n - 1u];

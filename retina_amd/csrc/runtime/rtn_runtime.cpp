@@ -14,17 +14,22 @@
 #include <vector>
 
 #include "../filtergen/codegen.hpp"
+#include "rtn_error.hpp"
+
+namespace {
+thread_local std::string g_err;
+}  // namespace
+
+int32_t rtn::set_error(int32_t code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
 
 namespace {
 
 #include "pc_kernel_src.inc"  // kPcKernelSrc: csrc/kernels/pc_kernel.hip as a string literal
 
-thread_local std::string g_err;
-
-int32_t fail(int32_t code, const std::string& msg) {
-  g_err = msg;
-  return code;
-}
+int32_t fail(int32_t code, const std::string& msg) { return rtn::set_error(code, msg); }
 
 size_t copy_text(const std::string& s, char* buf, size_t cap) {
   if (buf && cap > 0) {

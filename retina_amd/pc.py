@@ -39,6 +39,10 @@ class _Out(C.Structure):
                 ("counters", C.c_void_p)]
 
 
+class _PcapStats(C.Structure):
+    _fields_ = [("frames", C.c_uint64), ("skipped_mtu", C.c_uint64), ("packed", C.c_uint64), ("bytes", C.c_uint64)]
+
+
 class _Info(C.Structure):
     _fields_ = [("n_subscriptions", C.c_uint32), ("n_deliver_stmts", C.c_uint32),
                 ("deliver_words", C.c_uint32), ("tree_size", C.c_uint32)]
@@ -64,6 +68,13 @@ EXPORTS = {
     "rtn_out_l4_bytes": (C.c_size_t, [C.c_uint32]),
     "rtn_out_addr6_bytes": (C.c_size_t, [C.c_uint32]),
     "rtn_out_dlv_bytes": (C.c_size_t, [C.c_uint32, C.c_uint32]),
+    # include/retina_ingest.h
+    "rtn_pcap_open": (C.c_int32, [C.c_char_p, C.c_uint32, C.POINTER(C.c_void_p)]),
+    "rtn_pcap_next_batch": (C.c_int32, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint32,
+                                        C.POINTER(C.c_uint32)]),
+    "rtn_pcap_stats": (C.c_int32, [C.c_void_p, C.POINTER(_PcapStats)]),
+    "rtn_pcap_rewind": (C.c_int32, [C.c_void_p]),
+    "rtn_pcap_close": (None, [C.c_void_p]),
 }
 
 
@@ -300,3 +311,48 @@ def pack_frames(frames, stride: int = 128) -> tuple[np.ndarray, np.ndarray]:
         slab[i, :k] = b[:k]
         dlen[i] = len(b)
     return slab.reshape(-1), dlen
+
+
+class PcapReader:
+    """Offline ingest (include/retina_ingest.h): a libpcap/pcapng capture packed into the slot
+    layout rtn_pc_run reads, with the reference's offline-runtime rules (offline.rs:64-82)."""
+
+    def __init__(self, path, mtu: int = 9702):
+        h = C.c_void_p()
+        _check(lib().rtn_pcap_open(str(path).encode(), mtu, C.byref(h)))
+        self._h = h
+
+    def __del__(self):
+        if getattr(self, "_h", None) and self._h.value and _lib is not None:
+            _lib.rtn_pcap_close(self._h)
+            self._h = C.c_void_p()
+
+    def next_batch(self, slab: np.ndarray, stride: int, data_len: np.ndarray) -> int:
+        """Fill host arrays slab (uint8, >= cap*stride) and data_len (uint16[cap]); returns frames packed."""
+        cap = len(data_len)
+        assert slab.dtype == np.uint8 and data_len.dtype == np.uint16 and slab.size >= cap * stride
+        n = C.c_uint32()
+        _check(lib().rtn_pcap_next_batch(self._h, slab.ctypes.data, stride, data_len.ctypes.data, cap, C.byref(n)))
+        return n.value
+
+    def rewind(self) -> None:
+        _check(lib().rtn_pcap_rewind(self._h))
+
+    def stats(self) -> dict:
+        st = _PcapStats()
+        _check(lib().rtn_pcap_stats(self._h, C.byref(st)))
+        return {f: getattr(st, f) for f, _ in _PcapStats._fields_}
+
+    def read_all(self, stride: int = 128, batch: int = 1 << 16) -> tuple[np.ndarray, np.ndarray]:
+        slabs, lens = [], []
+        while True:
+            s = np.zeros(batch * stride, np.uint8)
+            d = np.zeros(batch, np.uint16)
+            k = self.next_batch(s, stride, d)
+            if k == 0:
+                break
+            slabs.append(s[:k * stride])
+            lens.append(d[:k])
+        if not slabs:
+            return np.zeros(0, np.uint8), np.zeros(0, np.uint16)
+        return np.concatenate(slabs), np.concatenate(lens)

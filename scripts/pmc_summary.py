@@ -24,7 +24,7 @@ KERNEL = "rtn_pc_kernel"
 
 def counter(path: Path) -> list[float]:
     rows = list(csv.DictReader(open(path)))
-    return [float(r["Counter_Value"]) for r in rows if KERNEL in r.get("Kernel_Name", "")]
+    return [float(r["Counter_Value"]) for r in rows if r.get("Kernel_Name", "").startswith(KERNEL)]
 
 
 def main(tag: str, cfg: str, frames: int) -> None:
@@ -34,12 +34,14 @@ def main(tag: str, cfg: str, frames: int) -> None:
     ks = out / f"prof_{tag}_{cfg}" / "run_kernel_stats.csv"
     shutil.copy(ks, prof / f"{tag}_{cfg}_kernel_stats.csv")
     stats = {r["Name"]: r for r in csv.DictReader(open(ks))}
-    k = stats[KERNEL]
+    # the dominant packet-stage kernel (rtn_pc_kernel_s64 for 64-byte slots, rtn_pc_kernel otherwise)
+    name = max((n for n in stats if n.startswith(KERNEL)), key=lambda n: float(stats[n]["TotalDurationNs"]))
+    k = stats[name]
     fetch = counter(out / f"pmc_{tag}_{cfg}_FETCH_SIZE" / "run_counter_collection.csv")
     write = counter(out / f"pmc_{tag}_{cfg}_WRITE_SIZE" / "run_counter_collection.csv")
     f_kb, w_kb = statistics.median(fetch), statistics.median(write)
     d = {
-        "tag": tag, "config": cfg, "frames": frames, "kernel": KERNEL,
+        "tag": tag, "config": cfg, "frames": frames, "kernel": name,
         "kernel_avg_ns": float(k["AverageNs"]), "kernel_calls": int(k["Calls"]),
         "fetch_size_kib_median": f_kb, "write_size_kib_median": w_kb, "pmc_dispatches": [len(fetch), len(write)],
         "read_bytes_per_launch": int(2 * f_kb * 1024), "write_bytes_per_launch": int(w_kb * 1024),

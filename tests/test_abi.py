@@ -1,5 +1,5 @@
 """The C-ABI library: loads on a machine without a GPU, exports every function declared in
-include/retina_pc.h, reports errors the way the header says, and its hiprtc path produces a
+include/*.h (retina_pc.h, retina_ingest.h), reports errors the way the header says, and its hiprtc path produces a
 gfx950 code object for every named subscription set (no GPU needed to compile)."""
 from __future__ import annotations
 
@@ -12,19 +12,21 @@ import pytest
 from golden.filter_sets import SETS
 from retina_amd import pc
 
-HEADER = Path(__file__).resolve().parent.parent / "include" / "retina_pc.h"
+HEADERS = sorted((Path(__file__).resolve().parent.parent / "include").glob("*.h"))
 
 
 def declared_functions() -> list[str]:
-    text = HEADER.read_text()
-    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return sorted(set(re.findall(r"\b(rtn_[a-z0-9_]+)\s*\(", text)))
+    names = set()
+    for h in HEADERS:
+        text = re.sub(r"/\*.*?\*/", "", h.read_text(), flags=re.S)
+        names |= set(re.findall(r"\b(rtn_[a-z0-9_]+)\s*\(", text))
+    return sorted(names)
 
 
 def test_exports_every_declared_symbol():
     lib = C.CDLL(str(pc._LIB_PATH))
     names = declared_functions()
-    assert len(names) >= 18
+    assert len(names) >= 23 and len(HEADERS) >= 2
     for n in names:
         assert hasattr(lib, n), n
     assert set(names) == set(pc.EXPORTS), set(names) ^ set(pc.EXPORTS)
