@@ -177,6 +177,9 @@ def main() -> None:
     ap.add_argument("--frames", type=int, default=0, help="frames per GPU (default: the config's)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--layout", choices=["auto", "mono", "split"], default="auto",
+                    help="slots wider than 64 B: monolithic, or split into 64-B head + 64-B ext slabs "
+                         "(auto = split; include/retina_pc.h)")
     args = ap.parse_args()
 
     import torch
@@ -199,7 +202,17 @@ def main() -> None:
     sh = rdist.shard(n, rank, world)  # weak scaling: a disjoint shard of the frame stream per rank
     slab, dlen = gen_frames(cfg, sh.count, start=sh.start)
     alg_bytes = synth.alg_read_bytes(slab, dlen, stride)
-    d_slab = torch.from_numpy(slab).to(dev)
+    split = stride > 64 and args.layout != "mono"
+    d_ext = None
+    if split:
+        head, ext = pc.split_slab(slab, stride)
+        d_slab = torch.from_numpy(head).to(dev)
+        d_ext = torch.from_numpy(ext).to(dev)
+        run_stride = 64
+        del head, ext
+    else:
+        d_slab = torch.from_numpy(slab).to(dev)
+        run_stride = stride
     d_dlen = torch.from_numpy(dlen.view(np.int16)).to(dev)
 
     prog = pc.Program.from_spec(spec_for(cfg))
@@ -208,7 +221,7 @@ def main() -> None:
     stream = torch.cuda.current_stream(dev)
 
     for _ in range(args.warmup):
-        ctx.run(d_slab, stride, d_dlen, n, out, stream=stream)
+        ctx.run(d_slab, run_stride, d_dlen, n, out, stream=stream, ext=d_ext)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -218,7 +231,7 @@ def main() -> None:
     t0 = time.perf_counter()
     ev0.record(stream)
     for _ in range(args.steps):
-        ctx.run(d_slab, stride, d_dlen, n, out, stream=stream)
+        ctx.run(d_slab, run_stride, d_dlen, n, out, stream=stream, ext=d_ext)
     ev1.record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -229,7 +242,7 @@ def main() -> None:
 
     # correctness totals of the last step (outside the timed region)
     cnt_out = ctx.alloc_outputs(n, addr6=True, counters=True)
-    ctx.run(d_slab, stride, d_dlen, n, cnt_out, stream=stream)
+    ctx.run(d_slab, run_stride, d_dlen, n, cnt_out, stream=stream, ext=d_ext)
     torch.cuda.synchronize(dev)
     counters = cnt_out.counters.view(torch.int32)[:3].to(torch.int64)
     stats = torch.tensor([wall, kern_ms], dtype=torch.float64, device=dev)
@@ -260,6 +273,7 @@ def main() -> None:
             "dtype": "u8",
             "data": "synthetic (seeded splitmix64 frames, retina_amd/synth.py)",
             "config": {"workload": f"{cfg}: {desc}", "frames_per_gpu": n, "stride": stride,
+                       "layout": "split (64-B head + 64-B ext slabs)" if split else f"{run_stride}-B slots",
                        "subscriptions": prog.info["n_subscriptions"], "tree_size": prog.info["tree_size"],
                        "parallelism": f"shard{world}"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

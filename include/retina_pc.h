@@ -63,27 +63,34 @@ typedef struct rtn_l4ctx {
 #define RTN_L4_FLAGS(m) (((m) >> 8) & 0xFFu)                       /* L4Context.flags (TCP)      */
 #define RTN_L4_LENGTH(m) ((m) >> 16)                               /* L4Context.length           */
 
-/* A batch of frames laid out for coalesced HBM reads: slot i (stride bytes, a multiple of 64)
- * holds the first min(data_len[i], stride) bytes of frame i. stride >= 128 is always valid;
- * stride 64 is valid when every data_len <= 64 (else counters[3] bit 0 is raised). */
+/* A batch of frames laid out for coalesced HBM reads, in one of two layouts:
+ *  - monolithic (ext == NULL): slot i (stride bytes, a multiple of 64) holds the first
+ *    min(data_len[i], stride) bytes of frame i;
+ *  - split (ext != NULL, stride == 64): slab slot i holds bytes [0, 64) of frame i and ext slot i
+ *    (64 bytes) bytes [64, 128). The kernel reads ext[i] only for frames whose headers run past
+ *    byte 64 (IPv6, IPv4 options, VLAN + options), so a frame costs 64 B of HBM reads unless it
+ *    needs more -- a 128-byte monolithic slot costs a whole 128-B line for every frame.
+ * A frame whose headers do not fit (stride 64 without ext) raises counters[3] bit 0. */
 typedef struct rtn_batch {
   const uint8_t* slab;
   uint64_t stride;
   const uint16_t* data_len; /* Mbuf::data_len of each frame (mbuf.rs:95-97) */
   uint32_t n;
   uint32_t core_id;         /* the calling lcore (passed to CoreId callbacks by the host) */
+  const uint8_t* ext;       /* split layout: bytes [64, 128) of each frame, 64-byte slots */
 } rtn_batch_t;
 
 /* Record arrays are dense per chunk of RTN_CHUNK_FRAMES frames, in frame order: the k-th
  * forwarded frame of chunk c = i / RTN_CHUNK_FRAMES has its L4Context at l4[c * RTN_CHUNK_FRAMES + k]
- * (k = popcount of fwd_bitmap over the chunk's frames before it); likewise addr6 (same index)
- * and dlv_records (ranked by dlv_bitmap). Bitmaps hold bit i % 64 of word i / 64 for frame i. */
+ * (k = popcount of fwd_bitmap over the chunk's frames before it); the j-th forwarded IPv6 frame
+ * of chunk c (records with RTN_L4_IPV6) has its addresses at addr6[c * RTN_CHUNK_FRAMES + j];
+ * dlv_records are ranked by dlv_bitmap the same way. Bitmaps hold bit i % 64 of word i / 64. */
 #define RTN_CHUNK_FRAMES 1024u
 typedef struct rtn_pc_out {
   uint64_t* pc_bitmap;   /* [ceil(n/64)]  Actions.data contains PacketContinue               */
   uint64_t* fwd_bitmap;  /* [ceil(n/64)]  ... and L4Context::new succeeded (goes to conntrack) */
   rtn_l4ctx_t* l4;       /* [ceil(n/1024)*1024] (rtn_out_l4_bytes); unused slots undefined    */
-  uint8_t* addr6;        /* optional [ceil(n/1024)*1024][32]: IPv6 src|dst bytes of IPv6 records */
+  uint8_t* addr6;        /* optional [ceil(n/1024)*1024][32]: src|dst of the IPv6 records   */
   uint64_t* dlv_bitmap;  /* [ceil(n/64)] frames with >= 1 packet-level callback (if any)     */
   uint64_t* dlv_records; /* [ceil(n/1024)*1024][1 + deliver_words]: frame index, statement mask */
   uint32_t* counters;    /* optional [4]: pc, fwd, dlv totals, status bits; zeroed per run

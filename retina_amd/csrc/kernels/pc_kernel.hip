@@ -81,6 +81,7 @@ struct rtn_args {
   rtn_u64* dlv_bm;            // [ceil(n/64)]  any packet-level delivery
   rtn_u64* dlv_recs;          // [ceil(n/64)*64][1 + RTN_DELIVER_WORDS]  (pkt_idx, statement mask words)
   rtn_u32* counters;          // [0] pc, [1] fwd, [2] dlv, [3] status bits
+  const unsigned char* ext;   // split layout: bytes 64..127 of each frame (64-byte slots), or null
 };
 
 struct rtn_view {
@@ -294,6 +295,7 @@ struct rtn_chunk {
   rtn_u64 rec_base;         // chunk * RTN_CHUNK_FRAMES
   rtn_u32 nrec, nflushed;   // records produced / already stored in this chunk
   rtn_u32 ndlv;             // delivery records produced in this chunk
+  rtn_u32 nv6, nv6flushed;  // IPv6 address records (addr6) produced / stored in this chunk
   rtn_u64 my_pc, my_fwd, my_dlv;  // lane k holds group k's bitmap words until the chunk ends
 };
 
@@ -321,12 +323,30 @@ __device__ __forceinline__ void rtn_flush(const rtn_args& a, const rtn_u64* ring
   }
 }
 
+// IPv6 address records (32 B: src, dst) are dense per chunk over the chunk's forwarded IPv6
+// frames. Where IPv6 is common (the split / wide-slot kernels) they leave through their own
+// per-wave LDS ring (128 entries, 4 KB) in whole 2-KB blocks: scattered 32-B stores with holes
+// between them cost about 4x their bytes in HBM time.
+#define RTN_RING6 128u
+#define RTN_FLUSH6 64u
+
+__device__ __forceinline__ void rtn_flush6(const rtn_args& a, const rtn_v4u* ring6, const rtn_chunk& ch, rtn_u32 lane,
+                                           rtn_u32 nent) {
+  const rtn_v4u* src = ring6 + (ch.nv6flushed & (RTN_RING6 - 1u)) * 2u;
+  rtn_v4u* dst = reinterpret_cast<rtn_v4u*>(a.addr6 + (ch.rec_base + ch.nv6flushed) * 32u);
+#pragma unroll
+  for (rtn_u32 j = 0; j < 2u; ++j) {
+    const rtn_u32 k = lane + 64u * j;
+    if (k < 2u * nent) RTN_ST(dst + k, src[k]);
+  }
+}
+
 // Everything after the slot's bytes arrived: parse, generated filter, L4Context, wave-level
 // compaction of the outputs of group g (the k-th group of the current chunk).
-template <int NW>
+template <int NW, bool STAGE6>
 __device__ __forceinline__ void rtn_group(const rtn_args& a, rtn_u32 g, rtn_u32 k, rtn_u32 lane, rtn_u64 lane_lt,
-                                          const rtn_u32 (&w)[NW], rtn_u32 dl, rtn_u64* ring, rtn_chunk& ch,
-                                          rtn_acc& acc) {
+                                          const rtn_u32 (&w)[NW], rtn_u32 dl, rtn_u64* ring, rtn_v4u* ring6,
+                                          rtn_chunk& ch, rtn_acc& acc) {
   const rtn_u32 i = g * 64u + lane;
   const bool valid = i < a.n;
   rtn_view v;
@@ -365,13 +385,35 @@ __device__ __forceinline__ void rtn_group(const rtn_args& a, rtn_u32 g, rtn_u32 
     rp[0] = (rtn_u64)src4 | ((rtn_u64)dst4 << 32);
     rp[1] = (rtn_u64)ports | ((rtn_u64)seq << 32);
     rp[2] = (rtn_u64)ack | ((rtn_u64)meta << 32);
-    if (v.v6 && (a.flags & 1u)) {
-      rtn_v4u* ap = reinterpret_cast<rtn_v4u*>(a.addr6 + (ch.rec_base + r) * 32u);
-      ap[0] = rtn_v4u{v.l3w[2], v.l3w[3], v.l3w[4], v.l3w[5]};
-      ap[1] = rtn_v4u{v.l3w[6], v.l3w[7], v.l3w[8], v.l3w[9]};
-    }
   }
   ch.nrec += nfwd;
+  // IPv6 source/destination addresses, ranked among the chunk's forwarded IPv6 frames
+#ifndef RTN_EXP_NO_ADDR6
+  const bool six = fwd && v.v6 && (a.flags & 1u);
+#else
+  const bool six = false;
+#endif
+  const rtn_u64 m6 = __ballot(six);
+  if (six) {
+    const rtn_u32 r6 = ch.nv6 + (rtn_u32)__popcll(m6 & lane_lt);
+    const rtn_v4u s0 = rtn_v4u{v.l3w[2], v.l3w[3], v.l3w[4], v.l3w[5]};
+    const rtn_v4u s1 = rtn_v4u{v.l3w[6], v.l3w[7], v.l3w[8], v.l3w[9]};
+    if (STAGE6) {
+      ring6[(r6 & (RTN_RING6 - 1u)) * 2u] = s0;
+      ring6[(r6 & (RTN_RING6 - 1u)) * 2u + 1u] = s1;
+    } else {
+      rtn_v4u* ap = reinterpret_cast<rtn_v4u*>(a.addr6 + (ch.rec_base + r6) * 32u);
+      ap[0] = s0;
+      ap[1] = s1;
+    }
+  }
+  ch.nv6 += (rtn_u32)__popcll(m6);
+  if (STAGE6 && ch.nv6 - ch.nv6flushed >= RTN_FLUSH6) {
+    rtn_wave_sync();
+    rtn_flush6(a, ring6, ch, lane, RTN_FLUSH6);
+    ch.nv6flushed += RTN_FLUSH6;
+    rtn_wave_sync();
+  }
   if (ch.nrec - ch.nflushed >= RTN_FLUSH) {  // pending < RTN_FLUSH + 64 <= RTN_RING: one block per group
     rtn_wave_sync();
     rtn_flush(a, ring, ch, lane, RTN_FLUSH);
@@ -388,7 +430,11 @@ __device__ __forceinline__ void rtn_group(const rtn_args& a, rtn_u32 g, rtn_u32 
     const rtn_u64 dlvm = __ballot(d);
     ch.my_dlv = lane == k ? dlvm : ch.my_dlv;
     acc.dlv += (rtn_u32)__popcll(dlvm);
+#ifdef RTN_EXP_NO_DLV
+    if (false) {
+#else
     if (d) {
+#endif
       const rtn_u64 slot_i = ch.rec_base + ch.ndlv + (rtn_u32)__popcll(dlvm & lane_lt);
       rtn_u64* dp = a.dlv_recs + slot_i * (1u + RTN_DELIVER_WORDS);
       dp[0] = (rtn_u64)i;
@@ -402,8 +448,12 @@ __device__ __forceinline__ void rtn_group(const rtn_args& a, rtn_u32 g, rtn_u32 
 
 // Chunk loop. Each wave takes chunks wave_g, wave_g + nwaves, ... and walks a chunk's groups in
 // order, RTN_UNROLL groups per iteration so that all of their loads are in flight before the
-// first is parsed.
-template <bool S64>
+// first is parsed. MODE: RTN_S64 (64-byte slots), RTN_SPLIT (64-byte slots + ext slab holding
+// bytes 64..127), RTN_MONO (monolithic slots of any stride >= 64).
+#define RTN_S64 0
+#define RTN_SPLIT 1
+#define RTN_MONO 2
+template <int MODE>
 __device__ __forceinline__ void rtn_run(const rtn_args& a) {
   const rtn_u32 lane = threadIdx.x & 63u;
   const rtn_u32 wave_g = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
@@ -411,9 +461,13 @@ __device__ __forceinline__ void rtn_run(const rtn_args& a) {
   const rtn_u32 nw = (a.n + 63u) >> 6;
   const rtn_u32 nchunks = (nw + RTN_CHUNK_GROUPS - 1u) / RTN_CHUNK_GROUPS;
   const rtn_u64 lane_lt = (lane == 0u) ? 0ull : (~0ull >> (64u - lane));
+  constexpr bool slots64 = MODE != RTN_MONO;
   rtn_acc acc = {0u, 0u, 0u, 0u};
   __shared__ __attribute__((aligned(16))) rtn_u64 rtn_ring[4][RTN_RING * 3u];
   rtn_u64* ring = rtn_ring[threadIdx.x >> 6];
+  constexpr bool stage6 = MODE != RTN_S64;  // 64-byte slots rarely forward IPv6 (only short UDP)
+  __shared__ __attribute__((aligned(16))) rtn_v4u rtn_ring6[4][stage6 ? RTN_RING6 * 2u : 1u];
+  rtn_v4u* ring6 = rtn_ring6[threadIdx.x >> 6];
 #ifdef RTN_XPOSE
   __shared__ __attribute__((aligned(16))) rtn_u32 rtn_tile[4][64 * RTN_XPITCH];
   rtn_u32* tile = rtn_tile[threadIdx.x >> 6];
@@ -421,12 +475,12 @@ __device__ __forceinline__ void rtn_run(const rtn_args& a) {
   for (rtn_u32 c = wave_g; c < nchunks; c += nwaves) {
     const rtn_u32 gb = c * RTN_CHUNK_GROUPS;
     const rtn_u32 ge = gb + RTN_CHUNK_GROUPS < nw ? gb + RTN_CHUNK_GROUPS : nw;
-    rtn_chunk ch = {(rtn_u64)c * (64u * RTN_CHUNK_GROUPS), 0u, 0u, 0u, 0ull, 0ull, 0ull};
+    rtn_chunk ch = {(rtn_u64)c * (64u * RTN_CHUNK_GROUPS), 0u, 0u, 0u, 0u, 0u, 0ull, 0ull, 0ull};
     for (rtn_u32 g0 = gb; g0 < ge; g0 += RTN_UNROLL) {
       rtn_u32 lo[RTN_UNROLL][16], dl[RTN_UNROLL];
 #ifdef RTN_XPOSE
       rtn_v4u q[RTN_UNROLL][4];
-      if (S64) {
+      if (slots64) {
 #pragma unroll
         for (int u = 0; u < RTN_UNROLL; ++u) {
           const rtn_u32 g = g0 + u;
@@ -441,15 +495,51 @@ __device__ __forceinline__ void rtn_run(const rtn_args& a) {
           if (u == 0 || g < ge) rtn_load_lo(a, g * 64u + lane, lo[u], dl[u]);
         }
       }
+#ifdef RTN_HI_EARLY
+      // experiment: transpose and issue every group's second-half loads before parsing any
+      rtn_u32 wh[RTN_UNROLL][16];
+      if (MODE != RTN_S64) {
+#pragma unroll
+        for (int u = 0; u < RTN_UNROLL; ++u) {
+          const rtn_u32 g = g0 + u;
+          if (u > 0 && g >= ge) break;
+#ifdef RTN_XPOSE
+          if (slots64) rtn_xpose(tile, lane, q[u], lo[u]);
+#endif
+#pragma unroll
+          for (int j = 0; j < 16; ++j) wh[u][j] = 0u;
+          if (rtn_need_hi(lo[u], dl[u])) {
+            const rtn_v4u* hi = MODE == RTN_SPLIT
+                                    ? reinterpret_cast<const rtn_v4u*>(a.ext + (rtn_u64)(g * 64u + lane) * 64u)
+                                    : reinterpret_cast<const rtn_v4u*>(a.slab + (rtn_u64)(g * 64u + lane) * a.stride) + 4;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const rtn_v4u x = RTN_LD(hi + j);
+              wh[u][4 * j + 0] = x.x; wh[u][4 * j + 1] = x.y; wh[u][4 * j + 2] = x.z; wh[u][4 * j + 3] = x.w;
+            }
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < RTN_UNROLL; ++u) {
+          const rtn_u32 g = g0 + u;
+          if (u > 0 && g >= ge) break;
+          rtn_u32 w[32];
+#pragma unroll
+          for (int j = 0; j < 16; ++j) { w[j] = lo[u][j]; w[16 + j] = wh[u][j]; }
+          rtn_group<32, stage6>(a, g, g - gb, lane, lane_lt, w, dl[u], ring, ring6, ch, acc);
+        }
+        continue;
+      }
+#endif
 #pragma unroll
       for (int u = 0; u < RTN_UNROLL; ++u) {
         const rtn_u32 g = g0 + u;
         if (u > 0 && g >= ge) break;
-        if (S64) {
 #ifdef RTN_XPOSE
-          rtn_xpose(tile, lane, q[u], lo[u]);
+        if (slots64) rtn_xpose(tile, lane, q[u], lo[u]);
 #endif
-          rtn_group<16>(a, g, g - gb, lane, lane_lt, lo[u], dl[u], ring, ch, acc);
+        if (MODE == RTN_S64) {
+          rtn_group<16, stage6>(a, g, g - gb, lane, lane_lt, lo[u], dl[u], ring, ring6, ch, acc);
         } else {
           rtn_u32 w[32];
 #pragma unroll
@@ -457,14 +547,17 @@ __device__ __forceinline__ void rtn_run(const rtn_args& a) {
 #pragma unroll
           for (int j = 16; j < 32; ++j) w[j] = 0u;
           if (rtn_need_hi(lo[u], dl[u])) {
-            const rtn_v4u* slot = reinterpret_cast<const rtn_v4u*>(a.slab + (rtn_u64)(g * 64u + lane) * a.stride);
+            // bytes 64..127: the ext slot (split layout) or the slot's second half (monolithic)
+            const rtn_v4u* hi = MODE == RTN_SPLIT
+                                    ? reinterpret_cast<const rtn_v4u*>(a.ext + (rtn_u64)(g * 64u + lane) * 64u)
+                                    : reinterpret_cast<const rtn_v4u*>(a.slab + (rtn_u64)(g * 64u + lane) * a.stride) + 4;
 #pragma unroll
-            for (int j = 4; j < 8; ++j) {
-              const rtn_v4u x = RTN_LD(slot + j);
-              w[4 * j + 0] = x.x; w[4 * j + 1] = x.y; w[4 * j + 2] = x.z; w[4 * j + 3] = x.w;
+            for (int j = 0; j < 4; ++j) {
+              const rtn_v4u x = RTN_LD(hi + j);
+              w[16 + 4 * j + 0] = x.x; w[16 + 4 * j + 1] = x.y; w[16 + 4 * j + 2] = x.z; w[16 + 4 * j + 3] = x.w;
             }
           }
-          rtn_group<32>(a, g, g - gb, lane, lane_lt, w, dl[u], ring, ch, acc);
+          rtn_group<32, stage6>(a, g, g - gb, lane, lane_lt, w, dl[u], ring, ring6, ch, acc);
         }
       }
     }
@@ -472,6 +565,7 @@ __device__ __forceinline__ void rtn_run(const rtn_args& a) {
 #ifndef RTN_EXP_NO_STORES
     rtn_wave_sync();
     rtn_flush(a, ring, ch, lane, ch.nrec - ch.nflushed);
+    if (stage6) rtn_flush6(a, ring6, ch, lane, ch.nv6 - ch.nv6flushed);
     rtn_wave_sync();
 #endif
     if (lane < ge - gb) {
@@ -531,8 +625,9 @@ __device__ __forceinline__ void rtn_lane_read(const rtn_args& a) {
 }
 #define RTN_BODY(S64) { rtn_lane_read(a); }
 #else
-#define RTN_BODY(S64) { rtn_run<S64>(a); }
+#define RTN_BODY(MODE) { rtn_run<MODE>(a); }
 #endif
 
-extern "C" __global__ void __launch_bounds__(256) rtn_pc_kernel(rtn_args a) RTN_BODY(false)
-extern "C" __global__ void __launch_bounds__(256) rtn_pc_kernel_s64(rtn_args a) RTN_BODY(true)
+extern "C" __global__ void __launch_bounds__(256) rtn_pc_kernel(rtn_args a) RTN_BODY(RTN_MONO)
+extern "C" __global__ void __launch_bounds__(256) rtn_pc_kernel_s64(rtn_args a) RTN_BODY(RTN_S64)
+extern "C" __global__ void __launch_bounds__(256) rtn_pc_kernel_split(rtn_args a) RTN_BODY(RTN_SPLIT)

@@ -121,6 +121,7 @@ struct KArgs {
   uint64_t* dlv_bm;
   uint64_t* dlv_recs;
   uint32_t* counters;
+  const unsigned char* ext;
 };
 
 }  // namespace
@@ -136,8 +137,9 @@ struct rtn_pc {
   const rtn_program* program = nullptr;
   int device = 0;
   hipModule_t module = nullptr;
-  hipFunction_t fn = nullptr;      // rtn_pc_kernel: any stride (multiple of 64)
-  hipFunction_t fn_s64 = nullptr;  // rtn_pc_kernel_s64: 64-byte slots
+  hipFunction_t fn = nullptr;        // rtn_pc_kernel: monolithic slots, any stride (multiple of 64)
+  hipFunction_t fn_s64 = nullptr;    // rtn_pc_kernel_s64: 64-byte slots
+  hipFunction_t fn_split = nullptr;  // rtn_pc_kernel_split: 64-byte slots + ext
   uint32_t blocks = 0;
   uint32_t* scratch_counters = nullptr;  // used when the caller passes no counters
 };
@@ -255,6 +257,8 @@ int32_t rtn_pc_create_from_program(rtn_program_t* p, int device, rtn_pc_t** out)
   if (e != hipSuccess) return fail(RTN_EDEVICE, std::string("hipModuleGetFunction: ") + hipGetErrorString(e));
   e = hipModuleGetFunction(&pc->fn_s64, pc->module, "rtn_pc_kernel_s64");
   if (e != hipSuccess) return fail(RTN_EDEVICE, std::string("hipModuleGetFunction: ") + hipGetErrorString(e));
+  e = hipModuleGetFunction(&pc->fn_split, pc->module, "rtn_pc_kernel_split");
+  if (e != hipSuccess) return fail(RTN_EDEVICE, std::string("hipModuleGetFunction: ") + hipGetErrorString(e));
   e = hipMalloc(&pc->scratch_counters, 16);
   if (e != hipSuccess) return fail(RTN_EDEVICE, std::string("hipMalloc: ") + hipGetErrorString(e));
   if (const char* g = getenv("RTN_GRID")) pc->blocks = (uint32_t)strtoul(g, nullptr, 10);
@@ -287,6 +291,9 @@ int32_t rtn_pc_run(rtn_pc_t* pc, const rtn_batch_t* in, rtn_pc_out_t* out, void*
   if (!in->slab || !in->data_len) return fail(RTN_EINVAL, "batch slab/data_len missing");
   if (in->stride < 64 || in->stride % 64 != 0) return fail(RTN_EINVAL, "stride must be a positive multiple of 64");
   if ((reinterpret_cast<uintptr_t>(in->slab) & 15u) != 0) return fail(RTN_EINVAL, "slab must be 16-byte aligned");
+  if (in->ext && in->stride != 64) return fail(RTN_EINVAL, "the split layout (ext) needs stride 64");
+  if (in->ext && (reinterpret_cast<uintptr_t>(in->ext) & 15u) != 0)
+    return fail(RTN_EINVAL, "ext must be 16-byte aligned");
   if (!out->pc_bitmap || !out->fwd_bitmap || !out->l4) return fail(RTN_EINVAL, "pc_bitmap/fwd_bitmap/l4 required");
   const uint32_t dw = pc->program->prog.deliver_words();
   if (dw > 0 && (!out->dlv_bitmap || !out->dlv_records))
@@ -310,13 +317,14 @@ int32_t rtn_pc_run(rtn_pc_t* pc, const rtn_batch_t* in, rtn_pc_out_t* out, void*
   a.dlv_bm = out->dlv_bitmap;
   a.dlv_recs = out->dlv_records;
   a.counters = out->counters ? out->counters : pc->scratch_counters;
+  a.ext = in->ext;
   const uint32_t chunks = (in->n + RTN_CHUNK_FRAMES - 1u) / RTN_CHUNK_FRAMES;
   uint32_t blocks = pc->blocks ? pc->blocks : 2048u;
   const uint32_t need = (chunks + 3u) / 4u;  // one wave per chunk at most
   if (blocks > need) blocks = need;
   if (blocks == 0) blocks = 1;
   void* params[] = {&a};
-  hipFunction_t fn = in->stride == 64 ? pc->fn_s64 : pc->fn;
+  hipFunction_t fn = in->ext ? pc->fn_split : (in->stride == 64 ? pc->fn_s64 : pc->fn);
   e = hipModuleLaunchKernel(fn, blocks, 1, 1, 256, 1, 1, 0, s, params, nullptr);
   if (e != hipSuccess) return fail(RTN_EDEVICE, std::string("hipModuleLaunchKernel: ") + hipGetErrorString(e));
   return RTN_OK;

@@ -30,7 +30,7 @@ class FilterError(RetinaError):
 
 class _Batch(C.Structure):
     _fields_ = [("slab", C.c_void_p), ("stride", C.c_uint64), ("data_len", C.c_void_p),
-                ("n", C.c_uint32), ("core_id", C.c_uint32)]
+                ("n", C.c_uint32), ("core_id", C.c_uint32), ("ext", C.c_void_p)]
 
 
 class _Out(C.Structure):
@@ -217,8 +217,12 @@ class PCOutputs:
         recs = decode_l4(recs_all[idx], np.nonzero(fwd)[0])
         out = {"pc": pc, "fwd": fwd, "l4": recs}
         if self.addr6 is not None:
+            # dense per chunk over the chunk's forwarded IPv6 frames; one row per record here
             a6 = self.addr6.cpu().numpy().view(np.uint8).reshape(-1, 32)
-            out["addr6"] = a6[idx]
+            v6 = recs["ver"] == 6
+            rows = np.zeros((len(recs), 32), np.uint8)
+            rows[v6] = a6[_rank_index(recs["pkt_idx"][v6].astype(np.int64))]
+            out["addr6"] = rows
         if self.deliver_words:
             dbm = self.dlv_bitmap.cpu().numpy().view(np.uint64)
             recs_d = self.dlv_records.cpu().numpy().view(np.uint64).reshape(-1, 1 + self.deliver_words)
@@ -230,17 +234,21 @@ class PCOutputs:
 CHUNK_FRAMES = 1024  # RTN_CHUNK_FRAMES (include/retina_pc.h)
 
 
-def _segment_index(bm: np.ndarray) -> np.ndarray:
-    """Record-array index of every set bit of `bm`, in frame order: records are dense per chunk
-    of CHUNK_FRAMES frames, starting at chunk * CHUNK_FRAMES."""
-    bits = np.unpackbits(bm.view(np.uint8), bitorder="little").astype(np.int64)
-    frames = np.nonzero(bits)[0]
+def _rank_index(frames: np.ndarray) -> np.ndarray:
+    """Record-array index of each of `frames` (ascending frame indices of one record stream):
+    records are dense per chunk of CHUNK_FRAMES frames, starting at chunk * CHUNK_FRAMES."""
     if frames.size == 0:
         return np.zeros(0, np.int64)
     chunk = frames // CHUNK_FRAMES
-    # rank within the chunk = number of set bits of the same chunk before it
+    # rank within the chunk = number of the stream's frames of the same chunk before it
     first = np.searchsorted(chunk, chunk, side="left")
     return chunk * CHUNK_FRAMES + (np.arange(frames.size, dtype=np.int64) - first)
+
+
+def _segment_index(bm: np.ndarray) -> np.ndarray:
+    """Record-array index of every set bit of `bm`, in frame order."""
+    bits = np.unpackbits(bm.view(np.uint8), bitorder="little").astype(np.int64)
+    return _rank_index(np.nonzero(bits)[0])
 
 
 class PacketContinue:
@@ -283,14 +291,17 @@ class PacketContinue:
         )
 
     def run(self, slab, stride: int, data_len, n: int | None = None, out: PCOutputs | None = None,
-            stream=None, core_id: int = 0) -> PCOutputs:
+            stream=None, core_id: int = 0, ext=None) -> PCOutputs:
+        """One rtn_pc_run. `ext` (device uint8, 64 B per frame) selects the split layout: `slab`
+        then holds bytes [0, 64) of every frame (stride 64) and `ext` bytes [64, 128)."""
         import torch
 
         if n is None:
             n = int(data_len.numel())
         if out is None or out.n < n:
             out = self.alloc_outputs(n)
-        b = _Batch(slab.data_ptr(), stride, data_len.data_ptr(), n, core_id)
+        b = _Batch(slab.data_ptr(), stride, data_len.data_ptr(), n, core_id,
+                   ext.data_ptr() if ext is not None else None)
         ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
         o = _Out(ptr(out.pc_bitmap), ptr(out.fwd_bitmap), ptr(out.l4), ptr(out.addr6), ptr(out.dlv_bitmap),
                  ptr(out.dlv_records), ptr(out.counters))
@@ -298,6 +309,12 @@ class PacketContinue:
         _check(lib().rtn_pc_run(self._h, C.byref(b), C.byref(o), C.c_void_p(s.cuda_stream)))
         out.n = n
         return out
+
+
+def split_slab(slab: np.ndarray, stride: int) -> tuple[np.ndarray, np.ndarray]:
+    """Monolithic slots of `stride` >= 128 -> the split layout (64-B head slots, 64-B ext slots)."""
+    b = slab.reshape(-1, stride)
+    return np.ascontiguousarray(b[:, :64]).reshape(-1), np.ascontiguousarray(b[:, 64:128]).reshape(-1)
 
 
 def pack_frames(frames, stride: int = 128) -> tuple[np.ndarray, np.ndarray]:

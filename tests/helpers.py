@@ -39,7 +39,9 @@ def oracle_run(spec: str, slab: np.ndarray, stride: int, dlen: np.ndarray) -> di
     return {"pc": r["pc"], "fwd": r["fwd"], "rec": rec, "dm": r["dm"]}
 
 
-def gpu_run(spec: str, slab: np.ndarray, stride: int, dlen: np.ndarray, device: int = 0) -> dict:
+def gpu_run(spec: str, slab: np.ndarray, stride: int, dlen: np.ndarray, device: int = 0, split: bool = False) -> dict:
+    """Run the product on the GPU. split=True hands the frames over in the split layout
+    (64-B head slots + 64-B ext slots, include/retina_pc.h) instead of `stride`-byte slots."""
     import torch
 
     from retina_amd import pc
@@ -48,9 +50,14 @@ def gpu_run(spec: str, slab: np.ndarray, stride: int, dlen: np.ndarray, device: 
     ctx = pc.PacketContinue(prog, device)
     dev = torch.device("cuda", device)
     n = len(dlen)
+    ext_t = None
+    if split:
+        head, ext = pc.split_slab(np.ascontiguousarray(slab, np.uint8), stride)
+        slab, stride = head, 64
+        ext_t = torch.from_numpy(ext).to(dev)
     slab_t = torch.from_numpy(np.ascontiguousarray(slab, np.uint8)).to(dev)
     dl_t = torch.from_numpy(np.ascontiguousarray(dlen, np.uint16).view(np.int16)).to(dev)
-    out = ctx.run(slab_t, stride, dl_t, n)
+    out = ctx.run(slab_t, stride, dl_t, n, ext=ext_t)
     torch.cuda.synchronize()
     d = out.decode()
     cnt = out.counters_host()

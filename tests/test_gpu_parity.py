@@ -29,26 +29,29 @@ def _corpus(name: str):
     return np.concatenate([s2, s3, s4]), np.concatenate([d2, d3, d4])
 
 
+@pytest.mark.parametrize("layout", ["mono", "split"])
 @pytest.mark.parametrize("corpus", ["traces", "adversarial", "synth"])
 @pytest.mark.parametrize("fset", list(SETS))
-def test_golden_fixture(fset, corpus, gpu):
+def test_golden_fixture(fset, corpus, layout, gpu):
     g = np.load(GOLD / f"golden_{fset}.npz")
     slab, dlen = _corpus(corpus)
     n = len(dlen)
     exp = {"pc": np.unpackbits(g[f"{corpus}_pc"])[:n].astype(bool),
            "fwd": np.unpackbits(g[f"{corpus}_fwd"])[:n].astype(bool),
            "rec": g[f"{corpus}_rec"], "dm": g[f"{corpus}_dm"]}
-    got = helpers.gpu_run(SETS[fset], slab, 128, dlen)
-    helpers.assert_same(got, exp, f"{fset}/{corpus}")
+    got = helpers.gpu_run(SETS[fset], slab, 128, dlen, split=layout == "split")
+    helpers.assert_same(got, exp, f"{fset}/{corpus}/{layout}")
 
 
-@pytest.mark.parametrize("cfg,stride", [("cfg2", 64), ("cfg3", 128), ("cfg4", 128)])
-def test_synthetic_vs_oracle(cfg, stride, gpu):
+@pytest.mark.parametrize("cfg,stride,split", [("cfg2", 64, False), ("cfg3", 128, False), ("cfg4", 128, False),
+                                              ("cfg3", 128, True), ("cfg4", 128, True)])
+def test_synthetic_vs_oracle(cfg, stride, split, gpu):
     n = (1 << 18) + 37  # ragged tail: not a multiple of 64
     gen = {"cfg2": synth.cfg2, "cfg3": synth.cfg3, "cfg4": synth.cfg4}[cfg]
     slab, dlen = gen(n, start=1 << 20)
     spec = SETS[cfg]
-    helpers.assert_same(helpers.gpu_run(spec, slab, stride, dlen), helpers.oracle_run(spec, slab, stride, dlen), cfg)
+    helpers.assert_same(helpers.gpu_run(spec, slab, stride, dlen, split=split),
+                        helpers.oracle_run(spec, slab, stride, dlen), f"{cfg}/split={split}")
 
 
 @pytest.mark.parametrize("fset", ["quirks", "payload", "port_count", "match_all", "basic"])
