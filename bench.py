@@ -177,6 +177,8 @@ def main() -> None:
     ap.add_argument("--frames", type=int, default=0, help="frames per GPU (default: the config's)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
+                    help="N>1 collectives: nccl (= RCCL over xGMI) or gloo (CPU; rehearsal)")
     ap.add_argument("--layout", choices=["auto", "mono", "split"], default="auto",
                     help="slots wider than 64 B: monolithic, or split into 64-B head + 64-B ext slabs "
                          "(auto = split; include/retina_pc.h)")
@@ -188,11 +190,18 @@ def main() -> None:
     from retina_amd import dist as rdist
 
     rank, world, local = rdist.env_rank()
+    # one process per GPU; --dist-backend gloo with more ranks than GPUs rehearses the N>1 path
+    # (barriers, max-over-ranks timing, totals reduction) on a single card
+    gpu = local % max(1, torch.cuda.device_count())
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+        torch.cuda.set_device(gpu)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group("gloo")
+    dev = torch.device("cuda", gpu)
     torch.cuda.set_device(dev)
+    local = gpu
 
     from retina_amd import pc, synth
 

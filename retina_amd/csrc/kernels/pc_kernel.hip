@@ -33,7 +33,7 @@ typedef unsigned int rtn_v4u __attribute__((ext_vector_type(4)));
 #define RTN_CHUNK_GROUPS 16u  // groups per output chunk: 1024 frames (RTN_CHUNK_FRAMES in retina_pc.h)
 #endif
 #ifndef RTN_UNROLL
-#define RTN_UNROLL 2  // groups per loop iteration per wave (loads of all of them in flight together)
+#define RTN_UNROLL 1  // groups per loop iteration per wave (2 measured no faster, 12 more VGPRs)
 #endif
 #if defined(RTN_SC1_STORES)
 #define RTN_ST(p, v) asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory")

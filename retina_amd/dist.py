@@ -38,8 +38,13 @@ def reduce_totals(totals, times):
     import torch.distributed as dist
 
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-        dist.all_reduce(totals, op=dist.ReduceOp.SUM)
-        dist.all_reduce(times, op=dist.ReduceOp.MAX)
+        host = dist.get_backend() == "gloo" and totals.is_cuda  # gloo reduces host tensors
+        t, m = (totals.cpu(), times.cpu()) if host else (totals, times)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        dist.all_reduce(m, op=dist.ReduceOp.MAX)
+        if host:
+            totals.copy_(t)
+            times.copy_(m)
     return totals, times
 
 
