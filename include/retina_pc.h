@@ -85,14 +85,14 @@ typedef struct rtn_batch {
  * (k = popcount of fwd_bitmap over the chunk's frames before it); the j-th forwarded IPv6 frame
  * of chunk c (records with RTN_L4_IPV6) has its addresses at addr6[c * RTN_CHUNK_FRAMES + j];
  * dlv_records are ranked by dlv_bitmap the same way. Bitmaps hold bit i % 64 of word i / 64. */
-#define RTN_CHUNK_FRAMES 1024u
+#define RTN_CHUNK_FRAMES 512u
 typedef struct rtn_pc_out {
   uint64_t* pc_bitmap;   /* [ceil(n/64)]  Actions.data contains PacketContinue               */
   uint64_t* fwd_bitmap;  /* [ceil(n/64)]  ... and L4Context::new succeeded (goes to conntrack) */
-  rtn_l4ctx_t* l4;       /* [ceil(n/1024)*1024] (rtn_out_l4_bytes); unused slots undefined    */
-  uint8_t* addr6;        /* optional [ceil(n/1024)*1024][32]: src|dst of the IPv6 records   */
+  rtn_l4ctx_t* l4;       /* [ceil(n/512)*512] (rtn_out_l4_bytes); unused slots undefined    */
+  uint8_t* addr6;        /* optional [ceil(n/512)*512][32]: src|dst of the IPv6 records   */
   uint64_t* dlv_bitmap;  /* [ceil(n/64)] frames with >= 1 packet-level callback (if any)     */
-  uint64_t* dlv_records; /* [ceil(n/1024)*1024][1 + deliver_words]: frame index, statement mask */
+  uint64_t* dlv_records; /* [ceil(n/512)*512][1 + deliver_words]: frame index, statement mask */
   uint32_t* counters;    /* optional [4]: pc, fwd, dlv totals, status bits; zeroed per run
                           (NULL: no totals, no memset -- the run is a single kernel launch) */
 } rtn_pc_out_t;

@@ -319,8 +319,10 @@ int32_t rtn_pc_run(rtn_pc_t* pc, const rtn_batch_t* in, rtn_pc_out_t* out, void*
   a.counters = out->counters ? out->counters : pc->scratch_counters;
   a.ext = in->ext;
   const uint32_t chunks = (in->n + RTN_CHUNK_FRAMES - 1u) / RTN_CHUNK_FRAMES;
-  uint32_t blocks = pc->blocks ? pc->blocks : 2048u;
-  const uint32_t need = (chunks + 3u) / 4u;  // one wave per chunk at most
+  // default: one wave per chunk (4 chunks per 256-thread block); the hardware dispatcher hands
+  // out blocks as earlier ones retire, which balances the tail better than a persistent grid
+  const uint32_t need = (chunks + 3u) / 4u;
+  uint32_t blocks = pc->blocks ? pc->blocks : need;
   if (blocks > need) blocks = need;
   if (blocks == 0) blocks = 1;
   void* params[] = {&a};

@@ -231,7 +231,7 @@ class PCOutputs:
         return out
 
 
-CHUNK_FRAMES = 1024  # RTN_CHUNK_FRAMES (include/retina_pc.h)
+CHUNK_FRAMES = 512  # RTN_CHUNK_FRAMES (include/retina_pc.h)
 
 
 def _rank_index(frames: np.ndarray) -> np.ndarray:

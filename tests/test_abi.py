@@ -66,7 +66,7 @@ def test_hiprtc_builds_gfx950_code_object(fset):
 def test_output_sizes():
     L = pc.lib()
     assert L.rtn_out_bitmap_bytes(65) == 16
-    assert L.rtn_out_l4_bytes(65) == 1024 * 24
-    assert L.rtn_out_l4_bytes(1025) == 2048 * 24
-    assert L.rtn_out_addr6_bytes(1) == 1024 * 32
-    assert L.rtn_out_dlv_bytes(64, 2) == 1024 * 3 * 8
+    assert L.rtn_out_l4_bytes(65) == 512 * 24
+    assert L.rtn_out_l4_bytes(1025) == 1536 * 24
+    assert L.rtn_out_addr6_bytes(1) == 512 * 32
+    assert L.rtn_out_dlv_bytes(64, 2) == 512 * 3 * 8
