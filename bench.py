@@ -177,6 +177,7 @@ def main() -> None:
     ap.add_argument("--frames", type=int, default=0, help="frames per GPU (default: the config's)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--no-conn", action="store_true", help="skip the connection-stage side measurement")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="N>1 collectives: nccl (= RCCL over xGMI) or gloo (CPU; rehearsal)")
     ap.add_argument("--layout", choices=["auto", "mono", "split"], default="auto",
@@ -249,6 +250,28 @@ def main() -> None:
     wall = time.perf_counter() - t0
     kern_ms = ev0.elapsed_time(ev1) / args.steps
 
+    # side measurement (not the bench value): the same step with the connection stage enabled
+    # (rtn_conn_t per forwarded frame: ConnId hash, creates bit, first-packet packet_filter)
+    conn_stage = None
+    if not args.no_conn and world == 1:
+        cout = ctx.alloc_outputs(n, addr6=True, counters=False, conn=True)
+        for _ in range(3):
+            ctx.run(d_slab, run_stride, d_dlen, n, cout, stream=stream, ext=d_ext)
+        c0 = torch.cuda.Event(enable_timing=True)
+        c1 = torch.cuda.Event(enable_timing=True)
+        c0.record(stream)
+        for _ in range(args.steps):
+            ctx.run(d_slab, run_stride, d_dlen, n, cout, stream=stream, ext=d_ext)
+        c1.record(stream)
+        torch.cuda.synchronize(dev)
+        cms = c0.elapsed_time(c1) / args.steps
+        conn_stage = {"kernel_ms": round(cms, 4), "mpps": round(n / cms / 1e3, 1),
+                      "vs_filter_only": round(kern_ms / cms, 3),
+                      "first_packet_tree_size": prog.info["conn_tree_size"],
+                      "note": "same step + rtn_conn_t (8 B) per forwarded frame: ConnId hash/orientation, "
+                              "creates bit, first-packet packet_filter actions"}
+        del cout
+
     # correctness totals of the last step (outside the timed region)
     cnt_out = ctx.alloc_outputs(n, addr6=True, counters=True)
     ctx.run(d_slab, run_stride, d_dlen, n, cnt_out, stream=stream, ext=d_ext)
@@ -292,6 +315,7 @@ def main() -> None:
             "cpu_baseline": cpu,
             "accepted": {"packet_continue": counters[0], "forwarded": counters[1], "delivered": counters[2]},
             "e2e_pcie": e2e,
+            "conn_stage": conn_stage,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -14,6 +14,11 @@
  *   - filtergen itself (filtergen/src/lib.rs:241-385, packet layer): rtn_program_compile turns a
  *     subscription spec (the #[subscription("spec.toml")] TOML format, filtergen/src/parse.rs)
  *     into a tree-specialised HIP kernel.
+ *   - optional connection stage of each forwarded frame (rtn_conn_t): the ConnId the conntrack
+ *     table is keyed by (conntrack/conn_id.rs:111-117) as a hash + orientation, whether the frame
+ *     may open a connection (Conn::new_tcp / new_udp, conntrack/conn/mod.rs:53-96), and the
+ *     generated first-packet `packet_filter` (FilterLayer::Packet, filtergen/src/lib.rs:284-285)
+ *     that ConnInfo::filter_first_packet runs for a new connection (conn/conn_info.rs:42-50).
  * The reference callers are core/src/lcore/rx_core.rs:117-141 (online) and
  * core/src/runtime/offline.rs:67-82 (pcap). See INTEGRATION.md for the Rust extern "C" binding.
  *
@@ -63,6 +68,27 @@ typedef struct rtn_l4ctx {
 #define RTN_L4_FLAGS(m) (((m) >> 8) & 0xFFu)                       /* L4Context.flags (TCP)      */
 #define RTN_L4_LENGTH(m) ((m) >> 16)                               /* L4Context.length           */
 
+/* Connection stage of a forwarded frame (8 bytes, indexed like its rtn_l4ctx_t):
+ *   hash  = rtn_conn_hash of the canonical ConnId: MurmurHash3-x86-32 block + finaliser steps,
+ *           seed 0x5EED, over the words [max ip (4 or 16 B as big-endian u32 words, most
+ *           significant first)], [min ip], (max port << 16 | min port), (proto | 0x100 if IPv6),
+ *           then h ^= 16 (IPv4) or 40 (IPv6) and fmix32. max/min are Rust's SocketAddr order
+ *           (ip, then port), as ConnId::new's cmp::max/min.
+ *   info  = packet_filter Actions.data (13 bits) | terminal_actions << 13 | creates << 26 |
+ *           src_is_max << 27 | any first-packet statement fired << 28. `creates`: the frame would
+ *           open a connection on a table miss (TCP SYN without ACK/RST, or any UDP). The
+ *           packet_filter result is that of this frame, which the host uses only when the frame
+ *           does open a connection. */
+typedef struct rtn_conn {
+  uint32_t hash;
+  uint32_t info;
+} rtn_conn_t;
+#define RTN_CONN_PF_DATA(i) ((i) & 0x1FFFu)
+#define RTN_CONN_PF_TERMINAL(i) (((i) >> 13) & 0x1FFFu)
+#define RTN_CONN_CREATES(i) (((i) >> 26) & 1u)
+#define RTN_CONN_SRC_IS_MAX(i) (((i) >> 27) & 1u)
+#define RTN_CONN_PF_STMTS(i) (((i) >> 28) & 1u)
+
 /* A batch of frames laid out for coalesced HBM reads, in one of two layouts:
  *  - monolithic (ext == NULL): slot i (stride bytes, a multiple of 64) holds the first
  *    min(data_len[i], stride) bytes of frame i;
@@ -95,6 +121,9 @@ typedef struct rtn_pc_out {
   uint64_t* dlv_records; /* [ceil(n/512)*512][1 + deliver_words]: frame index, statement mask */
   uint32_t* counters;    /* optional [4]: pc, fwd, dlv totals, status bits; zeroed per run
                           (NULL: no totals, no memset -- the run is a single kernel launch) */
+  rtn_conn_t* conn;      /* optional [ceil(n/512)*512]: connection stage, indexed like l4       */
+  uint64_t* conn_dlv;    /* [ceil(n/512)*512][conn_words] first-packet statement masks; required
+                          with conn when the program has first-packet statements           */
 } rtn_pc_out_t;
 
 typedef struct rtn_program_info {
@@ -102,7 +131,15 @@ typedef struct rtn_program_info {
   uint32_t n_deliver_stmts; /* packet-level callback sites in the generated code              */
   uint32_t deliver_words;   /* u64 words per statement mask (0 if no packet-level callbacks)  */
   uint32_t tree_size;       /* nodes of the collapsed PacketContinue tree                     */
+  uint32_t n_conn_stmts;    /* first-packet statement sites (FilterLayer::Packet)             */
+  uint32_t conn_words;      /* u64 words per first-packet statement mask                      */
+  uint32_t conn_tree_size;  /* nodes of the collapsed FilterLayer::Packet tree                */
 } rtn_program_info_t;
+
+/* What a first-packet statement does (the host runs it with its tracked connection data). */
+#define RTN_STMT_TRACKED_PACKETS 1u /* drain tracked.packets() into a packet-level callback */
+#define RTN_STMT_CALLBACK 2u        /* invoke a static/connection-level callback          */
+#define RTN_STMT_STREAM 3u          /* tracked.streaming_<id>.matched()                   */
 
 const char* rtn_last_error(void);
 
@@ -119,6 +156,14 @@ size_t rtn_program_source(const rtn_program_t* p, char* buf, size_t cap); /* ful
 /* Statement k of a deliver mask -> subscription index / Payload flag. */
 int32_t rtn_program_deliver_table(const rtn_program_t* p, uint32_t* sub_ids, uint8_t* is_payload,
                                   uint32_t cap);
+/* The first-packet filter (FilterLayer::Packet): its tree, its filtergen view, and statement
+ * k of a conn_dlv mask -> subscription index / RTN_STMT_* kind. */
+size_t rtn_program_conn_tree(const rtn_program_t* p, char* buf, size_t cap);
+size_t rtn_program_conn_rust(const rtn_program_t* p, char* buf, size_t cap);
+int32_t rtn_program_conn_table(const rtn_program_t* p, uint32_t* sub_ids, uint8_t* kinds, uint32_t cap);
+/* A collapsed tree as JSON (layer 0 = PacketContinue, 1 = Packet): nodes with pred, actions,
+ * deliver/stream subscription ids, if_else and children -- for tooling and the test oracle. */
+size_t rtn_program_tree_json(const rtn_program_t* p, uint32_t layer, char* buf, size_t cap);
 /* Compile the program's kernel for gfx950 (hiprtc; needs no GPU). Returns code-object bytes. */
 int32_t rtn_program_code_object(rtn_program_t* p, const uint8_t** data, size_t* len);
 void rtn_program_destroy(rtn_program_t* p);
@@ -137,6 +182,8 @@ size_t rtn_out_bitmap_bytes(uint32_t n);
 size_t rtn_out_l4_bytes(uint32_t n);
 size_t rtn_out_addr6_bytes(uint32_t n);
 size_t rtn_out_dlv_bytes(uint32_t n, uint32_t deliver_words);
+size_t rtn_out_conn_bytes(uint32_t n);
+size_t rtn_out_conn_dlv_bytes(uint32_t n, uint32_t conn_words);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,192 @@
+"""ORACLE (test infrastructure only): the connection stage of a forwarded frame.
+
+  core/src/conntrack/conn_id.rs:111-117    ConnId::new = (max(src, dst), min(src, dst), proto) in
+                                           Rust's SocketAddr order (ip as its integer, then port)
+  core/src/conntrack/conn/mod.rs:53-96     Conn::new_tcp opens a connection only on SYN without
+                                           ACK or RST; Conn::new_udp on any UDP frame
+  core/src/conntrack/conn/conn_info.rs:42-50  filter_first_packet -> the generated packet_filter
+  filtergen/src/packet_filter.rs:7-73      gen_packet_filter (FilterLayer::Packet): root body
+                                           first, first unary child `if`, later ones `else if`,
+                                           binary children by if_else, children before a node's
+                                           own body, Ethernet wrap iff the root has packet children
+  filtergen/src/utils.rs:251-285           update_body: actions, then delivers, then streams
+  include/retina_pc.h (rtn_conn_t)         the hash this repo defines over the canonical ConnId
+
+The FilterLayer::Packet tree itself is taken from the product compiler's JSON export
+(Program.tree_json(1)): the tree build is pinned by the reference's own ptree.rs KATs
+(tests/cpp/test_kats.cpp: core_ptree_packet, core_ptree_with_children, multi_ptree,
+core_ptree_prune), and what this module restates independently is its evaluation on the frame's
+bytes -- re-parsing the headers as packet_filter's parse_to chain does -- where the kernel
+evaluates it on the L4Context view it already holds.
+"""
+from __future__ import annotations
+
+from . import filterlang
+from .packet import Hdr, be, eval_binary, l4context, parse
+
+SYN, RST, ACK = 0x02, 0x04, 0x10  # core/src/protocols/packet/tcp.rs:13-20
+
+STMT_TRACKED_PACKETS, STMT_CALLBACK, STMT_STREAM = 1, 2, 3
+
+
+def _rotl(x: int, r: int) -> int:
+    return ((x << r) | (x >> (32 - r))) & 0xFFFFFFFF
+
+
+def _mix(h: int, k: int) -> int:
+    k = (k * 0xCC9E2D51) & 0xFFFFFFFF
+    k = _rotl(k, 15)
+    k = (k * 0x1B873593) & 0xFFFFFFFF
+    h ^= k
+    h = _rotl(h, 13)
+    return (h * 5 + 0xE6546B64) & 0xFFFFFFFF
+
+
+def _fmix(h: int) -> int:
+    h ^= h >> 16
+    h = (h * 0x85EBCA6B) & 0xFFFFFFFF
+    h ^= h >> 13
+    h = (h * 0xC2B2AE35) & 0xFFFFFFFF
+    return h ^ (h >> 16)
+
+
+def conn_hash(v6: bool, ip_max: int, ip_min: int, port_max: int, port_min: int, proto: int) -> int:
+    """rtn_conn_hash (include/retina_pc.h): MurmurHash3-x86-32 steps over the canonical words."""
+    nw = 4 if v6 else 1
+    h = 0x5EED
+    for ip in (ip_max, ip_min):
+        for j in range(nw - 1, -1, -1):
+            h = _mix(h, (ip >> (32 * j)) & 0xFFFFFFFF)
+    h = _mix(h, (port_max << 16) | port_min)
+    h = _mix(h, proto | (0x100 if v6 else 0))
+    return _fmix(h ^ (40 if v6 else 16))
+
+
+def conn_id(ctx) -> tuple[bool, tuple, tuple]:
+    """ConnId::new(src, dst, proto): (src_is_max, max endpoint, min endpoint). cmp::max returns
+    its second argument on equality, so src is the max endpoint only when strictly greater."""
+    src, dst = (ctx.src, ctx.sport), (ctx.dst, ctx.dport)
+    gt = src > dst
+    return gt, (src if gt else dst), (dst if gt else src)
+
+
+def creates(ctx) -> bool:
+    if ctx.proto == 17:
+        return True
+    return bool(ctx.flags & SYN) and not ctx.flags & ACK and not ctx.flags & RST
+
+
+class PacketFilter:
+    """The generated packet_filter for a FilterLayer::Packet tree (JSON nodes as exported by the
+    compiler); evaluate() runs it on one frame."""
+
+    def __init__(self, tree: dict, subs: list):
+        self.root = tree
+        self.subs = subs
+        self.stmts: list[tuple[int, int]] = []   # (sub id, STMT_*) in generated-code order
+        self._preds: dict[int, filterlang.Pred] = {}
+        self._number(tree, is_root=True)
+
+    def _pred(self, node: dict) -> filterlang.Pred:
+        if node["id"] not in self._preds:
+            dnf = filterlang.parse_filter(node["pred"])
+            assert len(dnf) == 1 and len(dnf[0]) == 1, node["pred"]
+            self._preds[node["id"]] = dnf[0][0]
+        return self._preds[node["id"]]
+
+    def _body_stmts(self, node: dict) -> list[int]:
+        ks = []
+        for sid in sorted(node["deliver"]):
+            kind = STMT_TRACKED_PACKETS if self.subs[sid].level == "Packet" else STMT_CALLBACK
+            ks.append(len(self.stmts))
+            self.stmts.append((sid, kind))
+        for sid in sorted(node["stream"]):
+            ks.append(len(self.stmts))
+            self.stmts.append((sid, STMT_STREAM))
+        return ks
+
+    def _root_has_body(self) -> bool:
+        r = self.root
+        return bool(r["data"] or r["terminal"] or r["deliver"])  # packet_filter.rs:15
+
+    def _number(self, node: dict, is_root: bool = False) -> None:
+        """Statement indices in code order: the root's body, then every child subtree (a child's
+        children before its own body)."""
+        if is_root:
+            node["_stmts"] = self._body_stmts(node) if self._root_has_body() else []
+            for c in node["children"]:
+                if filterlang.on_packet(self._pred(c)):
+                    self._number(c)
+            return
+        for c in node["children"]:
+            if filterlang.on_packet(self._pred(c)):
+                self._number(c)
+        node["_stmts"] = self._body_stmts(node)
+
+    def evaluate(self, frame: bytes, dl: int) -> tuple[int, int, list[int]]:
+        """(Actions.data, Actions.terminal, [fired statement index, ...])."""
+        d = bytes(frame) + bytes(max(0, 256 - len(frame)))
+        out = {"data": 0, "term": 0, "fired": []}
+
+        def body(node: dict):
+            out["data"] |= node["data"]
+            out["term"] |= node["terminal"]
+            out["fired"].extend(node["_stmts"])
+
+        def children(node: dict, env: dict):
+            chain_taken = False
+            first_unary = True
+            for c in node["children"]:
+                if not filterlang.on_packet(self._pred(c)):
+                    continue
+                if c["unary"]:
+                    cont = not first_unary
+                    first_unary = False
+                else:
+                    cont = c["if_else"]
+                if not cont:
+                    chain_taken = False
+                if chain_taken:
+                    continue
+                p = self._pred(c)
+                env2 = env
+                if c["unary"]:
+                    h = parse(d, dl, p.proto, env[node["protocol"]])
+                    ok = h is not None
+                    if ok:
+                        env2 = dict(env)
+                        env2[p.proto] = h
+                else:
+                    ok = eval_binary(d, env[p.proto], p)
+                if ok:
+                    chain_taken = True
+                    children(c, env2)
+                    body(c)
+
+        root = self.root
+        any_pkt = any(filterlang.on_packet(self._pred(c)) for c in root["children"])
+        has_body = self._root_has_body()
+        eth = parse(d, dl, "ethernet", None)
+        if (has_body or any_pkt) and any_pkt and eth is None:   # add_root_pred's Ethernet wrap
+            return 0, 0, []
+        if has_body:
+            body(root)
+        children(root, {"ethernet": eth})
+        return out["data"], out["term"], out["fired"]
+
+
+def stage(pf: PacketFilter, frame: bytes, dl: int) -> tuple[int, int, list[int]] | None:
+    """Connection stage of one frame: (hash, info, fired statements), or None if the frame is
+    not forwarded to conntrack (the caller checks the PacketContinue gate)."""
+    ctx = l4context(bytes(frame) + bytes(max(0, 256 - len(frame))), dl)
+    if ctx is None:
+        return None
+    gt, mx, mn = conn_id(ctx)
+    h = conn_hash(ctx.ver == 6, mx[0], mn[0], mx[1], mn[1], ctx.proto)
+    data, term, fired = pf.evaluate(frame, dl)
+    info = (data & 0x1FFF) | ((term & 0x1FFF) << 13) | (int(creates(ctx)) << 26) | (int(gt) << 27) | \
+        (int(bool(fired)) << 28)
+    return h, info, fired
+
+
+__all__ = ["PacketFilter", "stage", "conn_hash", "conn_id", "creates", "Hdr", "be"]

@@ -146,6 +146,19 @@ def on_packet(p: Pred) -> bool:
     return not (has_path(p.proto, "tcp") or has_path(p.proto, "udp"))
 
 
+CONN_PROTOCOLS = ("ipv4", "ipv6", "tcp", "udp")                      # protocols/stream/mod.rs:165-167
+CONN_FIELDS = ("src_addr", "dst_addr", "src_port", "dst_port")        # stream/conn/layer{3,4}.rs
+
+
+def req_packet(p: Pred) -> bool:
+    """Predicate::req_packet (ast.rs:118-133): needs the raw packet, not connection data."""
+    if not on_packet(p):
+        return False
+    if not p.unary:
+        return p.field not in ("port", "addr") and p.field not in CONN_FIELDS
+    return p.proto not in CONN_PROTOCOLS
+
+
 # ----------------------------------------------------------------------------------------------
 # is_excl / is_child (ast.rs:215-452 and helpers 455-832)
 
@@ -867,6 +880,22 @@ def validate(sub: Sub) -> None:
         raise FilterError("Must have one streamable datatype in streaming subscription")
     if lv.count("Session") > 1:
         raise FilterError("Multiple session-level datatypes in subscription")
+    check_after_packet_layer(sub)
+
+
+def check_after_packet_layer(sub: Sub) -> None:
+    """filtergen builds the FilterLayer::Packet tree for every subscription (lib.rs:284); its
+    add_pattern panics on a per-packet field (ptree.rs:406-415) in any pattern that is not
+    already resolved at PacketContinue (FlatPattern::is_prev_layer, pattern.rs:53-61: all of a
+    packet-level subscription's predicates on_packet), up to the first predicate of a later layer."""
+    for pat in filter_patterns(sub.filter):
+        if sub.level == "Packet" and all(on_packet(p) for p in pat):
+            continue
+        for p in pat:
+            if not on_packet(p):
+                break
+            if req_packet(p):
+                raise FilterError("Cannot access per-packet fields (e.g., TCP flags, length) after packet filter.")
 
 
 def load_spec(text: str) -> list[Sub]:

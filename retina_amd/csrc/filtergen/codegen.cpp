@@ -89,6 +89,20 @@ const std::map<std::string, FieldDef>& fields(const std::string& proto) {
   return none;
 }
 
+// The first-packet filter (FilterLayer::Packet) may only test connection-invariant fields: the
+// tree build rejects every other one (Predicate::req_packet, ast.rs:118-133; ptree.rs:406-415),
+// and those all live in the forwarded frame's L4Context. `c` is the kernel's rtn_cview.
+const std::map<std::string, FieldDef>& conn_fields(const std::string& proto) {
+  static const std::map<std::string, FieldDef> ipv4 = {{"src_addr", {FT::V4, "c.src4"}}, {"dst_addr", {FT::V4, "c.dst4"}}};
+  static const std::map<std::string, FieldDef> ipv6 = {{"src_addr", {FT::V6, "c.s6"}}, {"dst_addr", {FT::V6, "c.d6"}}};
+  static const std::map<std::string, FieldDef> l4 = {{"src_port", {FT::U16, "c.sport"}}, {"dst_port", {FT::U16, "c.dport"}}};
+  static const std::map<std::string, FieldDef> none;
+  if (proto == "ipv4") return ipv4;
+  if (proto == "ipv6") return ipv6;
+  if (proto == "tcp" || proto == "udp") return l4;
+  return none;
+}
+
 const char* camel(const std::string& p) {
   if (p == "ethernet") return "Ethernet";
   if (p == "ipv4") return "Ipv4";
@@ -114,6 +128,7 @@ std::string u32lit(uint64_t v) { return std::to_string(v) + "u"; }
 struct Gen {
   PacketProgram& prog;
   std::string hip, rust;
+  FilterLayer layer = FilterLayer::PacketContinue;
 
   [[noreturn]] void type_error(const Predicate& p, const std::string& why) {
     throw FilterError("filter does not type-check (" + p.str() + "): " + why);
@@ -121,9 +136,13 @@ struct Gen {
 
   // binary_to_tokens (utils.rs:18-249): returns {hip_expr, rust_expr}
   std::pair<std::string, std::string> binary(const Predicate& p) {
-    const auto& tab = fields(p.protocol);
+    const bool conn = layer == FilterLayer::Packet;
+    const auto& tab = conn ? conn_fields(p.protocol) : fields(p.protocol);
     auto it = tab.find(p.field);
-    if (it == tab.end()) type_error(p, "no method named `" + p.field + "` on `" + camel(p.protocol) + "`");
+    if (it == tab.end()) {
+      if (conn) throw FilterError("internal: per-packet field " + p.str() + " in the first-packet filter");
+      type_error(p, "no method named `" + p.field + "` on `" + camel(p.protocol) + "`");
+    }
     const FieldDef& fd = it->second;
     const std::string racc = p.protocol + "." + p.field + "()";
     const Value& val = p.value;
@@ -178,7 +197,8 @@ struct Gen {
         std::string conj;
         for (int k = 0; k < 4; ++k) {
           std::string word;
-          if (fd.type == FT::V6) word = "rtn_l3_be32(v, " + std::string(fd.hip) + " + " + std::to_string(4 * k) + ")";
+          if (fd.type == FT::V6 && conn) word = std::string(fd.hip) + "[" + std::to_string(k) + "]";
+          else if (fd.type == FT::V6) word = "rtn_l3_be32(v, " + std::string(fd.hip) + " + " + std::to_string(4 * k) + ")";
           else word = k == 3 ? std::string(fd.hip) : std::string("0u");
           std::string term = full ? "(" + word + " == " + u32lit(aw[k]) + ")"
                                   : "((" + word + " & " + u32lit(mw[k]) + ") == " + u32lit(nw[k]) + ")";
@@ -199,8 +219,12 @@ struct Gen {
 
   static std::string ind(int d) { return std::string(2 * d, ' '); }
 
-  // update_body (utils.rs:251-285) at the PacketContinue layer
+  // update_body (utils.rs:251-285)
   void update_body(const PNode& n, int d) {
+    if (layer == FilterLayer::Packet) {
+      update_body_conn(n, d);
+      return;
+    }
     if (!n.actions.drop()) {
       hip += ind(d) + "act |= " + u32lit(n.actions.data) + ";\n";
       rust += ind(d) + "result.push(Actions{data:" + std::to_string(n.actions.data) + ",terminal:" +
@@ -226,12 +250,40 @@ struct Gen {
       }
       if (ty != "ZcFrame" && ty != "Payload") throw FilterError("unsupported packet datatype " + ty);
       uint32_t k = (uint32_t)prog.delivers.size();
-      prog.delivers.push_back(DeliverStmt{(uint32_t)dv.id, ty == "Payload", spec.callback});
+      prog.delivers.push_back(DeliverStmt{(uint32_t)dv.id, ty == "Payload", spec.callback, DeliverKind::Packet});
       std::string bit = "dm[" + std::to_string(k / 64) + "] |= (1ull << " + std::to_string(k % 64) + ");";
       if (ty == "Payload") hip += ind(d) + "if (v.payload_ok) { " + bit + " }\n";
       else hip += ind(d) + bit + "\n";
       rust += ind(d) + "if let Some(p) = " + ty + "::from_mbuf(mbuf) { " + spec.callback + "(" + params + "); }\n";
     }
+  }
+
+  // update_body at FilterLayer::Packet: actions with their terminal half, then the statements
+  // the host runs with its tracked data (build_packet_callback's tracked-packet drain,
+  // data.rs:318-330; build_callback, data.rs:332-393; streaming `matched()`, utils.rs:277-283)
+  // recorded as statement-mask bits in code order.
+  void update_body_conn(const PNode& n, int d) {
+    if (!n.actions.drop()) {
+      hip += ind(d) + "data |= " + u32lit(n.actions.data) + "; term |= " + u32lit(n.actions.terminal) + ";\n";
+      rust += ind(d) + "result.push(Actions{data:" + std::to_string(n.actions.data) + ",terminal:" +
+              std::to_string(n.actions.terminal) + "});\n";
+    }
+    auto stmt = [&](uint32_t sub, DeliverKind kind, const std::string& rust_stmt) {
+      uint32_t k = (uint32_t)prog.conn_delivers.size();
+      prog.conn_delivers.push_back(DeliverStmt{sub, false, prog.subs.at(sub).callback, kind});
+      hip += ind(d) + "cm[" + std::to_string(k / 64) + "] |= (1ull << " + std::to_string(k % 64) + ");\n";
+      rust += ind(d) + rust_stmt + "\n";
+    };
+    for (auto& dv : n.deliver) {
+      const SubscriptionSpec& spec = prog.subs.at(dv.id);
+      if (spec.level == Level::Packet)
+        stmt((uint32_t)dv.id, DeliverKind::TrackedPackets,
+             "for mbuf in tracked.packets() { /* " + spec.callback + " */ }");
+      else
+        stmt((uint32_t)dv.id, DeliverKind::Callback, spec.callback + "(/* tracked */);");
+    }
+    for (auto& sv : n.stream)
+      stmt((uint32_t)sv.id, DeliverKind::Stream, "tracked.streaming_" + std::to_string(sv.id) + ".matched();");
   }
 
   // gen_packet_filter_util (packet_filter.rs:31-73)
@@ -242,10 +294,11 @@ struct Gen {
       if (c.pred.is_unary()) {
         const std::string& proto = c.pred.protocol;
         std::string cond;
-        if (proto == "ipv4") cond = "v.v4";
-        else if (proto == "ipv6") cond = "v.v6";
-        else if (proto == "tcp") cond = "v.tcp";
-        else if (proto == "udp") cond = "v.udp";
+        const char* vv = layer == FilterLayer::Packet ? "c." : "v.";
+        if (proto == "ipv4") cond = std::string(vv) + "v4";
+        else if (proto == "ipv6") cond = std::string(vv) + "v6";
+        else if (proto == "tcp") cond = std::string(vv) + "tcp";
+        else if (proto == "udp") cond = std::string(vv) + "udp";
         else throw FilterError("internal: unexpected packet protocol " + proto);
         hip += ind(d) + (first_unary ? "if (" : "else if (") + cond + ") {\n";
         rust += ind(d) + (first_unary ? "if let Ok(" : "else if let Ok(") + proto + ") = parse_to::<" + camel(proto) +
@@ -270,7 +323,13 @@ PacketProgram compile_packet_program(const std::vector<SubscriptionSpec>& subs) 
   PacketProgram prog;
   prog.subs = subs;
   for (auto& s : prog.subs) s.validate_spec();
+  // filtergen builds every layer's tree (filtergen/src/lib.rs:274-304) and rejects the program
+  // if any of them panics (e.g. a per-packet field in a connection-level filter, ptree.rs:406-415)
+  for (FilterLayer l : {FilterLayer::Protocol, FilterLayer::Session, FilterLayer::ConnectionDeliver,
+                        FilterLayer::PacketDeliver})
+    (void)filter_subtree(l, prog.subs);
   prog.tree = filter_subtree(FilterLayer::PacketContinue, prog.subs);
+  prog.conn_tree = filter_subtree(FilterLayer::Packet, prog.subs);
   const PNode& root = prog.tree.root;
   if (root.actions.terminal != 0) throw FilterError("internal: terminal actions at PacketContinue");
 
@@ -296,6 +355,22 @@ PacketProgram compile_packet_program(const std::vector<SubscriptionSpec>& subs) 
                   "  (void)v; (void)dm;\n" +
                   g.hip + "}\n";
   prog.rust_listing = "let mut result = Actions::new();\n" + g.rust + "result\n";
+
+  // packet_filter: the same emission (gen_packet_filter with FilterLayer::Packet), evaluated on a
+  // forwarded frame's L4Context view. Such a frame always parses as Ethernet, so add_root_pred's
+  // wrap is a no-op here.
+  Gen gc{prog, "", "", FilterLayer::Packet};
+  const PNode& croot = prog.conn_tree.root;
+  bool c_any_pkt = false;
+  for (auto& c : croot.children) c_any_pkt = c_any_pkt || c.pred.on_packet();
+  if (!croot.actions.drop() || !croot.deliver.empty()) gc.update_body(croot, 1);  // packet_filter.rs:15-17
+  gc.children(croot, 1);
+  prog.hip_conn_body =
+      "__device__ __forceinline__ void rtn_conn_filter(const rtn_cview& c, rtn_u32& data, rtn_u32& term, rtn_u64* cm) "
+      "{\n  (void)c; (void)cm;\n" + gc.hip + "}\n";
+  prog.rust_conn_listing = "let mut result = Actions::new();\n" +
+                           std::string(c_any_pkt ? "if let Ok(ethernet) = parse_to::<Ethernet>(mbuf) {\n" : "") + gc.rust +
+                           (c_any_pkt ? "}\n" : "") + "result\n";
   return prog;
 }
 

@@ -14,11 +14,20 @@
 
 namespace rtn {
 
-// One packet-level callback invocation site in the generated code, in code (= execution) order.
+// What a delivery statement of the generated code does (the host runs it when its bit is set).
+enum class DeliverKind : uint32_t {
+  Packet = 0,          // PacketContinue: `if let Some(p) = T::from_mbuf(mbuf) { cb(p, ..) }` (data.rs:306-317)
+  TrackedPackets = 1,  // Packet layer, packet-level sub: drain `tracked.packets()` into cb (data.rs:318-330)
+  Callback = 2,        // Packet layer, static/connection-level sub: build_callback (data.rs:332-393)
+  Stream = 3,          // Packet layer, streaming sub: `tracked.streaming_<id>.matched()` (utils.rs:277-283)
+};
+
+// One callback invocation site in the generated code, in code (= execution) order.
 struct DeliverStmt {
   uint32_t sub_id;       // subscription index in the spec
   bool payload;          // Payload datatype: fires only if the payload slice is readable
   std::string callback;  // callback name (for the host dispatcher)
+  DeliverKind kind = DeliverKind::Packet;
 };
 
 struct PacketProgram {
@@ -29,9 +38,16 @@ struct PacketProgram {
   std::string rust_listing; // the Rust the reference filtergen would emit (normalised), for review
   bool wraps_ethernet = false;
   uint32_t deliver_words() const { return (uint32_t)((delivers.size() + 63) / 64); }
+
+  // first-packet filter (FilterLayer::Packet, the generated `packet_filter`, filtergen/src/lib.rs:284-285)
+  PTree conn_tree{FilterLayer::Packet};
+  std::vector<DeliverStmt> conn_delivers;
+  std::string hip_conn_body;      // __device__ rtn_conn_filter(const rtn_cview&, data, term, cm)
+  std::string rust_conn_listing;
+  uint32_t conn_deliver_words() const { return (uint32_t)((conn_delivers.size() + 63) / 64); }
 };
 
-// Compile subscriptions into the PacketContinue program. Throws FilterError on any filter
+// Compile subscriptions into the PacketContinue program (and the first-packet filter). Throws FilterError on any filter
 // the reference would reject at compile time (parse errors, layer errors, type errors).
 PacketProgram compile_packet_program(const std::vector<SubscriptionSpec>& subs);
 

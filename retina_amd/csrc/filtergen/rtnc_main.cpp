@@ -1,6 +1,7 @@
 // rtnc: command-line front end of the filter compiler (the filtergen step, run ahead of time).
 //   rtnc <spec.toml> [--tree] [--rust] [--hip]
 //   rtnc --filter "<filter>" [--datatype ConnRecord] ...
+//   rtnc <spec.toml> --layers      every FilterLayer's collapsed tree (filtergen/src/lib.rs:274-304)
 #include <cstdio>
 #include <fstream>
 #include <iostream>
@@ -10,7 +11,7 @@
 
 int main(int argc, char** argv) {
   std::vector<rtn::SubscriptionSpec> subs;
-  bool tree = false, rust = false, hip = false;
+  bool tree = false, rust = false, hip = false, layers = false;
   std::string filter;
   std::vector<std::string> dts;
   std::string spec_path;
@@ -19,11 +20,12 @@ int main(int argc, char** argv) {
     if (a == "--tree") tree = true;
     else if (a == "--rust") rust = true;
     else if (a == "--hip") hip = true;
+    else if (a == "--layers") layers = true;
     else if (a == "--filter" && i + 1 < argc) filter = argv[++i];
     else if (a == "--datatype" && i + 1 < argc) dts.push_back(argv[++i]);
     else spec_path = a;
   }
-  if (!tree && !rust && !hip) tree = rust = true;
+  if (!tree && !rust && !hip && !layers) tree = rust = true;
   try {
     if (!spec_path.empty()) {
       std::ifstream f(spec_path);
@@ -43,6 +45,12 @@ int main(int argc, char** argv) {
         s.add_datatype(dt);
       }
       subs.push_back(s);
+    }
+    if (layers) {
+      for (auto l : {rtn::FilterLayer::PacketContinue, rtn::FilterLayer::Packet, rtn::FilterLayer::Protocol,
+                     rtn::FilterLayer::Session, rtn::FilterLayer::ConnectionDeliver, rtn::FilterLayer::PacketDeliver})
+        std::cout << rtn::filter_subtree(l, subs).pprint();
+      return 0;
     }
     auto prog = rtn::compile_packet_program(subs);
     if (tree) std::cout << prog.tree.pprint();

@@ -85,6 +85,8 @@ struct rtn_args {
   rtn_u64* dlv_recs;          // [ceil(n/64)*64][1 + RTN_DELIVER_WORDS]  (pkt_idx, statement mask words)
   rtn_u32* counters;          // [0] pc, [1] fwd, [2] dlv, [3] status bits
   const unsigned char* ext;   // split layout: bytes 64..127 of each frame (64-byte slots), or null
+  rtn_u64* conn;              // optional [ceil(n/512)*512] rtn_conn_t, indexed like recs (flags bit2)
+  rtn_u64* conn_dlv;          // [ceil(n/512)*512][RTN_CONN_WORDS] first-packet statement masks
 };
 
 struct rtn_view {
@@ -104,6 +106,42 @@ struct rtn_view {
 #define rtn_l4_be32(v, off) ((rtn_l4_be16(v, off) << 16) | rtn_l4_be16(v, (off) + 2))
 
 //@@RTN_FILTER@@
+
+#ifndef RTN_CONN_WORDS
+#define RTN_CONN_WORDS 0
+#endif
+#define RTN_CM_WORDS (RTN_CONN_WORDS > 0 ? RTN_CONN_WORDS : 1)
+
+// A forwarded frame as the first-packet filter sees it (FilterLayer::Packet may only test the
+// connection-invariant fields: ast.rs:118-133). Addresses and ports are host-order values.
+struct rtn_cview {
+  bool v4, v6, tcp, udp;
+  rtn_u32 src4, dst4;
+  rtn_u32 s6[4], d6[4];  // big-endian words of the IPv6 addresses, most significant first
+  rtn_u32 sport, dport;
+};
+
+//@@RTN_CONN_FILTER@@
+
+// ConnId::new (conntrack/conn_id.rs:115-117) orders the endpoints by Rust's SocketAddr order: ip
+// (as its big-endian integer), then port. Its hash (rtn_conn_hash in retina_pc.h) is MurmurHash3's
+// 32-bit block and finaliser steps over the canonical words (max endpoint first).
+__device__ __forceinline__ rtn_u32 rtn_rotl(rtn_u32 x, int r) { return (x << r) | (x >> (32 - r)); }
+__device__ __forceinline__ rtn_u32 rtn_mix(rtn_u32 h, rtn_u32 k) {
+  k *= 0xcc9e2d51u;
+  k = rtn_rotl(k, 15);
+  k *= 0x1b873593u;
+  h ^= k;
+  h = rtn_rotl(h, 13);
+  return h * 5u + 0xe6546b64u;
+}
+__device__ __forceinline__ rtn_u32 rtn_fmix(rtn_u32 h) {
+  h ^= h >> 16;
+  h *= 0x85ebca6bu;
+  h ^= h >> 13;
+  h *= 0xc2b2ae35u;
+  return h ^ (h >> 16);
+}
 
 __device__ __forceinline__ rtn_u32 rtn_alignbyte2(rtn_u32 hi, rtn_u32 lo) {
   return __builtin_amdgcn_alignbyte(hi, lo, 2u);
@@ -402,6 +440,66 @@ __device__ __forceinline__ void rtn_group(const rtn_args& a, rtn_u32 g, rtn_u32 
     rp[0] = (rtn_u64)src4 | ((rtn_u64)dst4 << 32);
     rp[1] = (rtn_u64)ports | ((rtn_u64)seq << 32);
     rp[2] = (rtn_u64)ack | ((rtn_u64)meta << 32);
+    if (a.flags & 4u) {
+      // Connection stage of the first packet (conntrack/mod.rs:80-169): ConnId, whether the frame
+      // may open a connection (Conn::new_tcp / new_udp, conn/mod.rs:53-96) and the generated
+      // packet_filter (ConnInfo::filter_first_packet, conn_info.rs:42-50) on this frame.
+      rtn_cview c;
+      c.v4 = v.v4;
+      c.v6 = v.v6;
+      c.tcp = tcp;
+      c.udp = !tcp;
+      c.src4 = src4;
+      c.dst4 = dst4;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        c.s6[j] = v.v6 ? rtn_l3_be32(v, 8 + 4 * j) : 0u;
+        c.d6[j] = v.v6 ? rtn_l3_be32(v, 24 + 4 * j) : 0u;
+      }
+      c.sport = ports & 0xffffu;
+      c.dport = ports >> 16;
+      rtn_u32 pdata = 0u, pterm = 0u;
+      rtn_u64 cm[RTN_CM_WORDS];
+#pragma unroll
+      for (int j = 0; j < RTN_CM_WORDS; ++j) cm[j] = 0ull;
+      rtn_conn_filter(c, pdata, pterm, cm);
+      // src > dst in SocketAddr order (V4 vs V4 or V6 vs V6 here): ip first, then port
+      bool gt = c.sport > c.dport;
+      if (v.v6) {
+#pragma unroll
+        for (int j = 3; j >= 0; --j) {
+          gt = c.s6[j] != c.d6[j] ? c.s6[j] > c.d6[j] : gt;
+        }
+      } else {
+        gt = src4 != dst4 ? src4 > dst4 : gt;
+      }
+      rtn_u32 h = 0x5EEDu;
+      if (v.v6) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) h = rtn_mix(h, gt ? c.s6[j] : c.d6[j]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) h = rtn_mix(h, gt ? c.d6[j] : c.s6[j]);
+      } else {
+        h = rtn_mix(h, gt ? src4 : dst4);
+        h = rtn_mix(h, gt ? dst4 : src4);
+      }
+      const rtn_u32 pmax = gt ? c.sport : c.dport, pmin = gt ? c.dport : c.sport;
+      h = rtn_mix(h, (pmax << 16) | pmin);
+      h = rtn_mix(h, (tcp ? 6u : 17u) | (v.v6 ? 0x100u : 0u));
+      h = rtn_fmix(h ^ (v.v6 ? 40u : 16u));
+      const rtn_u32 fl = tcp ? rtn_l4_b(v, 13) : 0u;
+      const bool creates = !tcp || ((fl & 0x02u) && !(fl & 0x10u) && !(fl & 0x04u));  // SYN, not ACK/RST
+      rtn_u64 anyc = 0ull;
+#pragma unroll
+      for (int j = 0; j < RTN_CM_WORDS; ++j) anyc |= cm[j];
+      const rtn_u32 info = (pdata & 0x1fffu) | ((pterm & 0x1fffu) << 13) | (creates ? 1u << 26 : 0u) |
+                           (gt ? 1u << 27 : 0u) | (anyc ? 1u << 28 : 0u);
+      a.conn[ch.rec_base + r] = (rtn_u64)h | ((rtn_u64)info << 32);
+#if RTN_CONN_WORDS > 0
+#pragma unroll
+      for (int j = 0; j < RTN_CONN_WORDS; ++j) a.conn_dlv[(ch.rec_base + r) * RTN_CONN_WORDS + j] = cm[j];
+#endif
+    }
   }
   ch.nrec += nfwd;
   // IPv6 source/destination addresses, ranked among the chunk's forwarded IPv6 frames

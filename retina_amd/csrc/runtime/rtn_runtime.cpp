@@ -44,7 +44,8 @@ std::string build_source(const rtn::PacketProgram& prog) {
   const std::string tpl = kPcKernelSrc;
   const std::string marker = "//@@RTN_FILTER@@";
   size_t at = tpl.find(marker);
-  std::string head = "#define RTN_DELIVER_WORDS " + std::to_string(prog.deliver_words()) + "\n";
+  std::string head = "#define RTN_DELIVER_WORDS " + std::to_string(prog.deliver_words()) + "\n" +
+                     "#define RTN_CONN_WORDS " + std::to_string(prog.conn_deliver_words()) + "\n";
   // Kernel variants for experiments (e.g. "RTN_NO_PREFETCH"); never set in production runs.
   if (const char* d = getenv("RTN_KERNEL_DEFINES")) {
     std::string all = d, tok;
@@ -57,7 +58,40 @@ std::string build_source(const rtn::PacketProgram& prog) {
       }
     }
   }
-  return head + tpl.substr(0, at) + prog.hip_body + tpl.substr(at + marker.size());
+  std::string src = head + tpl.substr(0, at) + prog.hip_body + tpl.substr(at + marker.size());
+  const std::string cmarker = "//@@RTN_CONN_FILTER@@";
+  size_t cat = src.find(cmarker);
+  return src.substr(0, cat) + prog.hip_conn_body + src.substr(cat + cmarker.size());
+}
+
+std::string json_str(const std::string& s) {
+  std::string o = "\"";
+  for (char c : s) {
+    if (c == '"' || c == '\\') o += '\\';
+    o += c;
+  }
+  return o + "\"";
+}
+
+std::string node_json(const rtn::PNode& n) {
+  std::string o = "{\"id\":" + std::to_string(n.id) + ",\"pred\":" + json_str(n.pred.str()) +
+                  ",\"unary\":" + (n.pred.is_unary() ? "true" : "false") + ",\"protocol\":" + json_str(n.pred.protocol) +
+                  ",\"data\":" + std::to_string(n.actions.data) + ",\"terminal\":" + std::to_string(n.actions.terminal) +
+                  ",\"if_else\":" + (n.if_else ? "true" : "false") + ",\"deliver\":[";
+  bool first = true;
+  for (auto& d : n.deliver) {
+    o += (first ? "" : ",") + std::to_string(d.id);
+    first = false;
+  }
+  o += "],\"stream\":[";
+  first = true;
+  for (auto& d : n.stream) {
+    o += (first ? "" : ",") + std::to_string(d.id);
+    first = false;
+  }
+  o += "],\"children\":[";
+  for (size_t k = 0; k < n.children.size(); ++k) o += (k ? "," : "") + node_json(n.children[k]);
+  return o + "]}";
 }
 
 uint64_t fnv1a(const std::string& s) {
@@ -122,6 +156,8 @@ struct KArgs {
   uint64_t* dlv_recs;
   uint32_t* counters;
   const unsigned char* ext;
+  rtn_conn_t* conn;
+  uint64_t* conn_dlv;
 };
 
 }  // namespace
@@ -204,6 +240,31 @@ int32_t rtn_program_info(const rtn_program_t* p, rtn_program_info_t* info) {
   info->n_deliver_stmts = (uint32_t)p->prog.delivers.size();
   info->deliver_words = p->prog.deliver_words();
   info->tree_size = (uint32_t)p->prog.tree.size;
+  info->n_conn_stmts = (uint32_t)p->prog.conn_delivers.size();
+  info->conn_words = p->prog.conn_deliver_words();
+  info->conn_tree_size = (uint32_t)p->prog.conn_tree.size;
+  return RTN_OK;
+}
+
+size_t rtn_program_conn_tree(const rtn_program_t* p, char* buf, size_t cap) {
+  return p ? copy_text(p->prog.conn_tree.pprint(), buf, cap) : 0;
+}
+size_t rtn_program_conn_rust(const rtn_program_t* p, char* buf, size_t cap) {
+  return p ? copy_text(p->prog.rust_conn_listing, buf, cap) : 0;
+}
+size_t rtn_program_tree_json(const rtn_program_t* p, uint32_t layer, char* buf, size_t cap) {
+  if (!p || layer > 1) return 0;
+  return copy_text(node_json(layer == 0 ? p->prog.tree.root : p->prog.conn_tree.root), buf, cap);
+}
+
+int32_t rtn_program_conn_table(const rtn_program_t* p, uint32_t* sub_ids, uint8_t* kinds, uint32_t cap) {
+  if (!p) return fail(RTN_EINVAL, "null program");
+  const auto& d = p->prog.conn_delivers;
+  if (cap < d.size()) return fail(RTN_ERANGE, "statement table capacity too small");
+  for (size_t k = 0; k < d.size(); ++k) {
+    if (sub_ids) sub_ids[k] = d[k].sub_id;
+    if (kinds) kinds[k] = (uint8_t)d[k].kind;
+  }
   return RTN_OK;
 }
 
@@ -298,6 +359,8 @@ int32_t rtn_pc_run(rtn_pc_t* pc, const rtn_batch_t* in, rtn_pc_out_t* out, void*
   const uint32_t dw = pc->program->prog.deliver_words();
   if (dw > 0 && (!out->dlv_bitmap || !out->dlv_records))
     return fail(RTN_EINVAL, "program has packet-level callbacks: dlv_bitmap/dlv_records required");
+  if (out->conn && pc->program->prog.conn_deliver_words() > 0 && !out->conn_dlv)
+    return fail(RTN_EINVAL, "program has first-packet statements: conn_dlv required with conn");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   hipError_t e;
   if (out->counters) {
@@ -309,7 +372,7 @@ int32_t rtn_pc_run(rtn_pc_t* pc, const rtn_batch_t* in, rtn_pc_out_t* out, void*
   a.stride = in->stride;
   a.dlen = in->data_len;
   a.n = in->n;
-  a.flags = (out->addr6 ? 1u : 0u) | (out->counters ? 2u : 0u);
+  a.flags = (out->addr6 ? 1u : 0u) | (out->counters ? 2u : 0u) | (out->conn ? 4u : 0u);
   a.pc_bm = out->pc_bitmap;
   a.fwd_bm = out->fwd_bitmap;
   a.recs = out->l4;
@@ -318,6 +381,8 @@ int32_t rtn_pc_run(rtn_pc_t* pc, const rtn_batch_t* in, rtn_pc_out_t* out, void*
   a.dlv_recs = out->dlv_records;
   a.counters = out->counters ? out->counters : pc->scratch_counters;
   a.ext = in->ext;
+  a.conn = out->conn;
+  a.conn_dlv = out->conn_dlv;
   const uint32_t chunks = (in->n + RTN_CHUNK_FRAMES - 1u) / RTN_CHUNK_FRAMES;
   // default: one wave per chunk (4 chunks per 256-thread block); the hardware dispatcher hands
   // out blocks as earlier ones retire, which balances the tail better than a persistent grid
@@ -349,5 +414,8 @@ size_t rtn_out_addr6_bytes(uint32_t n) { return chunked(n) * 32u; }
 size_t rtn_out_dlv_bytes(uint32_t n, uint32_t deliver_words) {
   return chunked(n) * (1u + deliver_words) * 8u;
 }
+static_assert(sizeof(rtn_conn_t) == 8, "rtn_conn_t is 8 bytes");
+size_t rtn_out_conn_bytes(uint32_t n) { return chunked(n) * sizeof(rtn_conn_t); }
+size_t rtn_out_conn_dlv_bytes(uint32_t n, uint32_t conn_words) { return chunked(n) * conn_words * 8u; }
 
 }  // extern "C"

@@ -36,7 +36,7 @@ class _Batch(C.Structure):
 class _Out(C.Structure):
     _fields_ = [("pc_bitmap", C.c_void_p), ("fwd_bitmap", C.c_void_p), ("l4", C.c_void_p),
                 ("addr6", C.c_void_p), ("dlv_bitmap", C.c_void_p), ("dlv_records", C.c_void_p),
-                ("counters", C.c_void_p)]
+                ("counters", C.c_void_p), ("conn", C.c_void_p), ("conn_dlv", C.c_void_p)]
 
 
 class _PcapStats(C.Structure):
@@ -45,7 +45,8 @@ class _PcapStats(C.Structure):
 
 class _Info(C.Structure):
     _fields_ = [("n_subscriptions", C.c_uint32), ("n_deliver_stmts", C.c_uint32),
-                ("deliver_words", C.c_uint32), ("tree_size", C.c_uint32)]
+                ("deliver_words", C.c_uint32), ("tree_size", C.c_uint32), ("n_conn_stmts", C.c_uint32),
+                ("conn_words", C.c_uint32), ("conn_tree_size", C.c_uint32)]
 
 
 EXPORTS = {
@@ -57,6 +58,10 @@ EXPORTS = {
     "rtn_program_rust": (C.c_size_t, [C.c_void_p, C.c_char_p, C.c_size_t]),
     "rtn_program_source": (C.c_size_t, [C.c_void_p, C.c_char_p, C.c_size_t]),
     "rtn_program_deliver_table": (C.c_int32, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32]),
+    "rtn_program_conn_tree": (C.c_size_t, [C.c_void_p, C.c_char_p, C.c_size_t]),
+    "rtn_program_conn_rust": (C.c_size_t, [C.c_void_p, C.c_char_p, C.c_size_t]),
+    "rtn_program_conn_table": (C.c_int32, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32]),
+    "rtn_program_tree_json": (C.c_size_t, [C.c_void_p, C.c_uint32, C.c_char_p, C.c_size_t]),
     "rtn_program_code_object": (C.c_int32, [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]),
     "rtn_program_destroy": (None, [C.c_void_p]),
     "rtn_pc_create": (C.c_int32, [C.c_char_p, C.c_size_t, C.c_int, C.POINTER(C.c_void_p)]),
@@ -68,6 +73,8 @@ EXPORTS = {
     "rtn_out_l4_bytes": (C.c_size_t, [C.c_uint32]),
     "rtn_out_addr6_bytes": (C.c_size_t, [C.c_uint32]),
     "rtn_out_dlv_bytes": (C.c_size_t, [C.c_uint32, C.c_uint32]),
+    "rtn_out_conn_bytes": (C.c_size_t, [C.c_uint32]),
+    "rtn_out_conn_dlv_bytes": (C.c_size_t, [C.c_uint32, C.c_uint32]),
     # include/retina_ingest.h
     "rtn_pcap_open": (C.c_int32, [C.c_char_p, C.c_uint32, C.POINTER(C.c_void_p)]),
     "rtn_pcap_next_batch": (C.c_int32, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint32,
@@ -182,6 +189,33 @@ class Program:
         _check(lib().rtn_program_deliver_table(self._h, subs.ctypes.data, pay.ctypes.data, max(n, 1)))
         return subs[:n], pay[:n]
 
+    @property
+    def conn_tree(self) -> str:
+        """The collapsed FilterLayer::Packet tree (the first-packet `packet_filter`)."""
+        return _text(lib().rtn_program_conn_tree, self._h)
+
+    @property
+    def conn_rust(self) -> str:
+        return _text(lib().rtn_program_conn_rust, self._h)
+
+    def conn_table(self) -> tuple[np.ndarray, np.ndarray]:
+        """First-packet statement k -> (subscription index, RTN_STMT_* kind)."""
+        n = self.info["n_conn_stmts"]
+        subs = np.zeros(max(n, 1), np.uint32)
+        kinds = np.zeros(max(n, 1), np.uint8)
+        _check(lib().rtn_program_conn_table(self._h, subs.ctypes.data, kinds.ctypes.data, max(n, 1)))
+        return subs[:n], kinds[:n]
+
+    def tree_json(self, layer: int) -> dict:
+        """Collapsed tree of layer 0 (PacketContinue) or 1 (Packet) as nested dicts."""
+        import json
+
+        L = lib()
+        n = L.rtn_program_tree_json(self._h, layer, None, 0)
+        buf = C.create_string_buffer(n + 1)
+        L.rtn_program_tree_json(self._h, layer, buf, n + 1)
+        return json.loads(buf.value.decode())
+
     def code_object(self) -> bytes:
         p = C.c_void_p()
         n = C.c_size_t()
@@ -201,6 +235,9 @@ class PCOutputs:
     dlv_records: object
     counters: object
     deliver_words: int
+    conn: object = None
+    conn_dlv: object = None
+    conn_words: int = 0
 
     def counters_host(self) -> np.ndarray:
         return self.counters.cpu().numpy().view(np.uint32)
@@ -223,6 +260,13 @@ class PCOutputs:
             rows = np.zeros((len(recs), 32), np.uint8)
             rows[v6] = a6[_rank_index(recs["pkt_idx"][v6].astype(np.int64))]
             out["addr6"] = rows
+        if self.conn is not None:
+            c = self.conn.cpu().numpy().view(np.uint32).reshape(-1, 2)[idx]
+            out["conn_hash"] = c[:, 0].copy()
+            out["conn_info"] = c[:, 1].copy()
+            if self.conn_words:
+                cd = self.conn_dlv.cpu().numpy().view(np.uint64).reshape(-1, self.conn_words)
+                out["conn_dlv"] = cd[idx]
         if self.deliver_words:
             dbm = self.dlv_bitmap.cpu().numpy().view(np.uint64)
             recs_d = self.dlv_records.cpu().numpy().view(np.uint64).reshape(-1, 1 + self.deliver_words)
@@ -262,6 +306,7 @@ class PacketContinue:
         _check(lib().rtn_pc_create_from_program(program._h, device, C.byref(h)))
         self._h = h
         self.deliver_words = program.info["deliver_words"]
+        self.conn_words = program.info["conn_words"]
 
     def __del__(self):
         if getattr(self, "_h", None) and self._h.value and _lib is not None:
@@ -271,7 +316,7 @@ class PacketContinue:
     def set_grid(self, blocks: int) -> None:
         _check(lib().rtn_pc_set_grid(self._h, blocks))
 
-    def alloc_outputs(self, n: int, addr6: bool = True, counters: bool = True) -> PCOutputs:
+    def alloc_outputs(self, n: int, addr6: bool = True, counters: bool = True, conn: bool = False) -> PCOutputs:
         import torch
 
         dev = torch.device("cuda", self.device)
@@ -288,6 +333,9 @@ class PacketContinue:
             dlv_records=u8(L.rtn_out_dlv_bytes(n, dw)) if dw else None,
             counters=torch.zeros(16, dtype=torch.uint8, device=dev) if counters else None,
             deliver_words=dw,
+            conn=u8(L.rtn_out_conn_bytes(n)) if conn else None,
+            conn_dlv=u8(L.rtn_out_conn_dlv_bytes(n, self.conn_words)) if conn and self.conn_words else None,
+            conn_words=self.conn_words if conn else 0,
         )
 
     def run(self, slab, stride: int, data_len, n: int | None = None, out: PCOutputs | None = None,
@@ -304,7 +352,7 @@ class PacketContinue:
                    ext.data_ptr() if ext is not None else None)
         ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
         o = _Out(ptr(out.pc_bitmap), ptr(out.fwd_bitmap), ptr(out.l4), ptr(out.addr6), ptr(out.dlv_bitmap),
-                 ptr(out.dlv_records), ptr(out.counters))
+                 ptr(out.dlv_records), ptr(out.counters), ptr(out.conn), ptr(out.conn_dlv))
         s = stream if stream is not None else torch.cuda.current_stream(self.device)
         _check(lib().rtn_pc_run(self._h, C.byref(b), C.byref(o), C.c_void_p(s.cuda_stream)))
         out.n = n

@@ -184,10 +184,12 @@ def cfg4(n: int, start: int = 0, seed: int = 0x5EED0004, stride: int = 128):
 
 
 def _toml(subs) -> str:
+    """[[subscriptions]] entries from (filter, datatypes, callback[, streaming]) tuples."""
     out = []
-    for f, dts, cb in subs:
+    for f, dts, cb, *rest in subs:
         d = ", ".join(f'"{x}"' for x in dts)
-        out.append(f'[[subscriptions]]\nfilter = "{f}"\ndatatypes = [{d}]\ncallback = "{cb}"\n')
+        st = f'streaming = "{rest[0]}"\n' if rest else ""
+        out.append(f'[[subscriptions]]\nfilter = "{f}"\ndatatypes = [{d}]\ncallback = "{cb}"\n{st}')
     return "\n".join(out)
 
 

@@ -15,7 +15,7 @@ QUIRKS_SUBS = [
     ("ipv6.next_header = 6 and ipv6.hop_limit = 64", ["ZcFrame"], "i_cb"),
     ("tcp.synack = 1 and tcp.data_offset > 5", ["ZcFrame"], "j_cb"),
     ("ipv4.df = 0.0.0.1", ["ZcFrame"], "k_cb"),
-    ("ipv4.protocol = 17 and udp.length < 30", ["SessionList"], "l_cb"),
+    ("ipv4.protocol = 17 and udp.length < 30", ["ZcFrame"], "l_cb"),
     ("ipv6.src_addr != 2001:db8::/32", ["ConnRecord"], "m_cb"),
 ]
 
@@ -28,6 +28,19 @@ PAYLOAD_SUBS = [
 PORT_COUNT_SUBS = [("udp", ["ZcFrame", "CoreId"], "udp_cb"), ("tcp", ["ZcFrame", "CoreId"], "tcp_cb"),
                    ("tcp or udp", ["ConnRecord"], "conn_cb")]
 
+# the connection stage (first-packet packet_filter): static-level subscriptions delivered inside
+# packet_filter, connection/session-level actions, a streaming subscription, IPv6 prefixes
+CONN_SUBS = [
+    ("ipv4.src_addr = 10.0.0.0/8 and tcp.dst_port = 80", ["FiveTuple"], "ft_cb"),
+    ("tcp.port = 443", ["ConnRecord"], "conn_cb"),
+    ("ipv6.dst_addr = 2001:db8::/32 and udp", ["FiveTuple", "FilterStr"], "v6_cb"),
+    ("tls", ["TlsHandshake"], "tls_cb"),
+    ("tcp.src_port >= 1024 and ipv4.dst_addr != 10.0.0.0/8", ["ConnRecord"], "hi_cb"),
+    ("udp.port = 53", ["PktCount", "FiveTuple"], "dns_stream_cb", "packets=1"),
+    ("tcp.dst_port = 25", ["ZcFrame"], "smtp_pkt"),
+    ("ipv6.src_addr = ::1/128 or ipv4.addr = 192.168.0.0/16", ["FiveTuple"], "local_cb"),
+]
+
 MATCH_ALL_SUBS = [("", ["ZcFrame"], "all_cb"), ("", ["ConnRecord"], "conn_cb")]
 
 SETS = {
@@ -39,4 +52,5 @@ SETS = {
     "payload": synth._toml(PAYLOAD_SUBS),
     "port_count": synth._toml(PORT_COUNT_SUBS),
     "match_all": synth._toml(MATCH_ALL_SUBS),
+    "conn": synth._toml(CONN_SUBS),
 }

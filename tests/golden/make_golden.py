@@ -8,7 +8,9 @@
   golden_<set>.npz    expected outputs for every named subscription set (filter_sets.py) over
                       three corpora (traces, adversarial, synthetic cfg2/3/4 samples): the
                       PacketContinue bit, the forwarded bit, the L4Context of forwarded frames and
-                      the packet-level callback statement masks.
+                      the packet-level callback statement masks; and the connection stage of every
+                      forwarded frame (oracle/conn.py: ConnId hash and orientation, the creates
+                      bit, the first-packet packet_filter actions and statement masks).
 Expected outputs come from the C oracle and are cross-checked frame by frame against the
 independent pure-Python oracle (oracle/packet.py) before being written.
 """
@@ -25,7 +27,7 @@ sys.path.insert(0, str(ROOT))
 sys.path.insert(0, str(ROOT / "tests"))
 sys.path.insert(0, str(HERE))
 
-from oracle import filterlang, packet, pcap  # noqa: E402
+from oracle import conn, filterlang, packet, pcap  # noqa: E402
 from retina_amd import pc as rpc, synth  # noqa: E402
 
 import corpus  # noqa: E402
@@ -82,6 +84,24 @@ def python_crosscheck(spec: str, slab: np.ndarray, dlen: np.ndarray, res: dict, 
         assert (ctx is not None) == bool(res["fwd"][i]), (spec, i)
 
 
+def conn_expected(spec: str, slab: np.ndarray, dlen: np.ndarray, fwd: np.ndarray) -> tuple[np.ndarray, np.ndarray]:
+    """Connection stage of the forwarded frames, in frame order: (hash, info) and statement masks."""
+    prog = rpc.Program.from_spec(spec)
+    pf = conn.PacketFilter(prog.tree_json(1), filterlang.load_spec(spec))
+    words = max(1, (len(pf.stmts) + 63) // 64)
+    b = slab.reshape(-1, STRIDE)
+    idx = np.nonzero(fwd)[0]
+    hi = np.zeros((len(idx), 2), np.uint32)
+    cdm = np.zeros((len(idx), words), np.uint64)
+    for j, i in enumerate(idx):
+        r = conn.stage(pf, b[i].tobytes(), int(dlen[i]))
+        assert r is not None, (spec, i)
+        hi[j] = r[0], r[1]
+        for k in r[2]:
+            cdm[j, k // 64] |= np.uint64(1 << (k % 64))
+    return hi, cdm
+
+
 def main() -> None:
     ref = Path("/root/reference")
     if ref.exists():
@@ -97,6 +117,7 @@ def main() -> None:
             out[f"{cname}_fwd"] = np.packbits(r["fwd"])
             out[f"{cname}_rec"] = r["rec"]
             out[f"{cname}_dm"] = r["dm"]
+            out[f"{cname}_conn"], out[f"{cname}_cdm"] = conn_expected(spec, slab, dlen, r["fwd"])
         np.savez_compressed(HERE / f"golden_{name}.npz", **out)
         print(name, {k: int(np.unpackbits(v).sum()) for k, v in out.items() if k.endswith("_pc")})
     np.savez_compressed(HERE / "corpus_adversarial.npz", slab=cs["adversarial"][0], dlen=cs["adversarial"][1])

@@ -39,9 +39,11 @@ def oracle_run(spec: str, slab: np.ndarray, stride: int, dlen: np.ndarray) -> di
     return {"pc": r["pc"], "fwd": r["fwd"], "rec": rec, "dm": r["dm"]}
 
 
-def gpu_run(spec: str, slab: np.ndarray, stride: int, dlen: np.ndarray, device: int = 0, split: bool = False) -> dict:
+def gpu_run(spec: str, slab: np.ndarray, stride: int, dlen: np.ndarray, device: int = 0, split: bool = False,
+            conn: bool = False) -> dict:
     """Run the product on the GPU. split=True hands the frames over in the split layout
-    (64-B head slots + 64-B ext slots, include/retina_pc.h) instead of `stride`-byte slots."""
+    (64-B head slots + 64-B ext slots, include/retina_pc.h) instead of `stride`-byte slots;
+    conn=True also computes the connection stage (rtn_conn_t per forwarded frame)."""
     import torch
 
     from retina_amd import pc
@@ -57,7 +59,7 @@ def gpu_run(spec: str, slab: np.ndarray, stride: int, dlen: np.ndarray, device: 
         ext_t = torch.from_numpy(ext).to(dev)
     slab_t = torch.from_numpy(np.ascontiguousarray(slab, np.uint8)).to(dev)
     dl_t = torch.from_numpy(np.ascontiguousarray(dlen, np.uint16).view(np.int16)).to(dev)
-    out = ctx.run(slab_t, stride, dl_t, n, ext=ext_t)
+    out = ctx.run(slab_t, stride, dl_t, n, out=ctx.alloc_outputs(max(n, 1), conn=conn), ext=ext_t)
     torch.cuda.synchronize()
     d = out.decode()
     cnt = out.counters_host()
@@ -79,7 +81,31 @@ def gpu_run(spec: str, slab: np.ndarray, stride: int, dlen: np.ndarray, device: 
     if nd:
         dl = d["dlv"]
         dm[dl[:, 0].astype(np.int64)] = dl[:, 1:]
-    return {"pc": d["pc"], "fwd": d["fwd"], "rec": rec, "dm": dm, "counters": cnt, "program": prog}
+    res = {"pc": d["pc"], "fwd": d["fwd"], "rec": rec, "dm": dm, "counters": cnt, "program": prog}
+    if conn:
+        res["conn"] = np.stack([d["conn_hash"], d["conn_info"]], 1) if len(l4) else np.zeros((0, 2), np.uint32)
+        cw = prog.info["conn_words"]
+        res["cdm"] = d["conn_dlv"] if cw else np.zeros((len(l4), 1), np.uint64)
+    return res
+
+
+def oracle_conn(spec: str, slab: np.ndarray, stride: int, dlen: np.ndarray, fwd: np.ndarray):
+    """Connection stage of the forwarded frames from oracle/conn.py, in frame order."""
+    from oracle import conn as oconn
+    from retina_amd import pc
+
+    pf = oconn.PacketFilter(pc.Program.from_spec(spec).tree_json(1), subs_from_spec(spec))
+    words = max(1, (len(pf.stmts) + 63) // 64)
+    b = np.ascontiguousarray(slab, np.uint8).reshape(-1, stride)
+    idx = np.nonzero(fwd)[0]
+    hi = np.zeros((len(idx), 2), np.uint32)
+    cdm = np.zeros((len(idx), words), np.uint64)
+    for j, i in enumerate(idx):
+        h, info, fired = oconn.stage(pf, b[i].tobytes(), int(dlen[i]))
+        hi[j] = h, info
+        for k in fired:
+            cdm[j, k // 64] |= np.uint64(1 << (k % 64))
+    return hi, cdm
 
 
 def assert_same(gpu: dict, ora: dict, what: str = "") -> None:
