@@ -291,7 +291,7 @@ __device__ __forceinline__ void rtn_load_lo(const rtn_args& a, rtn_u32 i, rtn_u3
 // 64-byte slots, coalesced: the group's 4 KB arrive as four full-width 16-B-per-lane loads
 // (lane l of load k holds quarter l%4 of slot 16k + l/4) and an LDS tile (80-B pitch, conflict-
 // free ds_read_b128) turns them back into one slot per lane.
-#define RTN_XPITCH 20u
+#define RTN_XPITCH 16u  // one 64-B slot per row, 16-B chunks XOR-swizzled by (row >> 2) & 3
 __device__ __forceinline__ void rtn_load_group(const rtn_args& a, rtn_u32 g, rtn_u32 lane, rtn_v4u (&q)[4], rtn_u32& dl) {
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
@@ -307,11 +307,12 @@ __device__ __forceinline__ void rtn_xpose(rtn_u32* tile, rtn_u32 lane, const rtn
   rtn_wave_sync();
 #pragma unroll
   for (int k = 0; k < 4; ++k)
-    *reinterpret_cast<rtn_v4u*>(tile + (16u * k + (lane >> 2)) * RTN_XPITCH + (lane & 3u) * 4u) = q[k];
+    *reinterpret_cast<rtn_v4u*>(tile + (16u * k + (lane >> 2)) * RTN_XPITCH +
+                                ((lane & 3u) ^ ((lane >> 4) & 3u)) * 4u) = q[k];
   rtn_wave_sync();
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const rtn_v4u x = *reinterpret_cast<const rtn_v4u*>(tile + lane * RTN_XPITCH + 4u * j);
+    const rtn_v4u x = *reinterpret_cast<const rtn_v4u*>(tile + lane * RTN_XPITCH + ((j ^ (lane >> 2)) & 3u) * 4u);
     w[4 * j + 0] = x.x; w[4 * j + 1] = x.y; w[4 * j + 2] = x.z; w[4 * j + 3] = x.w;
   }
 }
@@ -351,8 +352,15 @@ struct rtn_chunk {
 #define RTN_FLUSH 128u
 #endif
 
-__device__ __forceinline__ void rtn_flush(const rtn_args& a, const rtn_u64* ring, const rtn_chunk& ch, rtn_u32 lane,
-                                          rtn_u32 nrecs) {
+__device__ __forceinline__ void rtn_flush(const rtn_args& a, const rtn_u64* ring, const rtn_u64* cring,
+                                          const rtn_chunk& ch, rtn_u32 lane, rtn_u32 nrecs) {
+  if (a.flags & 4u) {
+    // connection-stage entries (8 B) share the records' indices: same block, 128-B lines
+    const rtn_u32 nc = ((nrecs + 1u) / 2u + 7u) & ~7u;
+    const rtn_v4u* csrc = reinterpret_cast<const rtn_v4u*>(cring + (ch.nflushed & (RTN_RING - 1u)));
+    rtn_v4u* cdst = reinterpret_cast<rtn_v4u*>(a.conn + ch.rec_base + ch.nflushed);
+    if (lane < nc) RTN_ST(cdst + lane, csrc[lane]);
+  }
 #ifndef RTN_NO_PAD_TAIL
   // whole 128-B lines only: the block starts line-aligned and the tail is padded with stale ring
   // bytes into the chunk's unused record space (a partial line costs a read-modify-write)
@@ -400,8 +408,8 @@ __device__ __forceinline__ void rtn_flush6(const rtn_args& a, const rtn_v4u* rin
 // compaction of the outputs of group g (the k-th group of the current chunk).
 template <int NW, bool STAGE6>
 __device__ __forceinline__ void rtn_group(const rtn_args& a, rtn_u32 g, rtn_u32 k, rtn_u32 lane, rtn_u64 lane_lt,
-                                          const rtn_u32 (&w)[NW], rtn_u32 dl, rtn_u64* ring, rtn_v4u* ring6,
-                                          rtn_chunk& ch, rtn_acc& acc) {
+                                          const rtn_u32 (&w)[NW], rtn_u32 dl, rtn_u64* ring, rtn_u64* cring,
+                                          rtn_v4u* ring6, rtn_chunk& ch, rtn_acc& acc) {
   const rtn_u32 i = g * 64u + lane;
   const bool valid = i < a.n;
   rtn_view v;
@@ -494,7 +502,7 @@ __device__ __forceinline__ void rtn_group(const rtn_args& a, rtn_u32 g, rtn_u32 
       for (int j = 0; j < RTN_CM_WORDS; ++j) anyc |= cm[j];
       const rtn_u32 info = (pdata & 0x1fffu) | ((pterm & 0x1fffu) << 13) | (creates ? 1u << 26 : 0u) |
                            (gt ? 1u << 27 : 0u) | (anyc ? 1u << 28 : 0u);
-      a.conn[ch.rec_base + r] = (rtn_u64)h | ((rtn_u64)info << 32);
+      cring[r & (RTN_RING - 1u)] = (rtn_u64)h | ((rtn_u64)info << 32);
 #if RTN_CONN_WORDS > 0
 #pragma unroll
       for (int j = 0; j < RTN_CONN_WORDS; ++j) a.conn_dlv[(ch.rec_base + r) * RTN_CONN_WORDS + j] = cm[j];
@@ -531,7 +539,7 @@ __device__ __forceinline__ void rtn_group(const rtn_args& a, rtn_u32 g, rtn_u32 
   }
   if (ch.nrec - ch.nflushed >= RTN_FLUSH) {  // pending < RTN_FLUSH + 64 <= RTN_RING: one block per group
     rtn_wave_sync();
-    rtn_flush(a, ring, ch, lane, RTN_FLUSH);
+    rtn_flush(a, ring, cring, ch, lane, RTN_FLUSH);
     ch.nflushed += RTN_FLUSH;
     rtn_wave_sync();
   }
@@ -580,6 +588,8 @@ __device__ __forceinline__ void rtn_run(const rtn_args& a) {
   rtn_acc acc = {0u, 0u, 0u, 0u};
   __shared__ __attribute__((aligned(16))) rtn_u64 rtn_ring[4][RTN_RING * 3u];
   rtn_u64* ring = rtn_ring[threadIdx.x >> 6];
+  __shared__ __attribute__((aligned(16))) rtn_u64 rtn_cring[4][RTN_RING];  // connection-stage entries
+  rtn_u64* cring = rtn_cring[threadIdx.x >> 6];
   constexpr bool stage6 = MODE != RTN_S64;  // 64-byte slots rarely forward IPv6 (only short UDP)
   __shared__ __attribute__((aligned(16))) rtn_v4u rtn_ring6[4][stage6 ? RTN_RING6 * 2u : 1u];
   rtn_v4u* ring6 = rtn_ring6[threadIdx.x >> 6];
@@ -641,7 +651,7 @@ __device__ __forceinline__ void rtn_run(const rtn_args& a) {
           rtn_u32 w[32];
 #pragma unroll
           for (int j = 0; j < 16; ++j) { w[j] = lo[u][j]; w[16 + j] = wh[u][j]; }
-          rtn_group<32, stage6>(a, g, g - gb, lane, lane_lt, w, dl[u], ring, ring6, ch, acc);
+          rtn_group<32, stage6>(a, g, g - gb, lane, lane_lt, w, dl[u], ring, cring, ring6, ch, acc);
         }
         continue;
       }
@@ -661,7 +671,7 @@ __device__ __forceinline__ void rtn_run(const rtn_args& a) {
           for (int j = 0; j < 16; ++j) x ^= lo[u][j];
           acc.status |= (x == 0x9E3779B9u) ? 2u : 0u;
 #else
-          rtn_group<16, stage6>(a, g, g - gb, lane, lane_lt, lo[u], dl[u], ring, ring6, ch, acc);
+          rtn_group<16, stage6>(a, g, g - gb, lane, lane_lt, lo[u], dl[u], ring, cring, ring6, ch, acc);
 #endif
         } else {
           rtn_u32 w[32];
@@ -680,14 +690,14 @@ __device__ __forceinline__ void rtn_run(const rtn_args& a) {
               w[16 + 4 * j + 0] = x.x; w[16 + 4 * j + 1] = x.y; w[16 + 4 * j + 2] = x.z; w[16 + 4 * j + 3] = x.w;
             }
           }
-          rtn_group<32, stage6>(a, g, g - gb, lane, lane_lt, w, dl[u], ring, ring6, ch, acc);
+          rtn_group<32, stage6>(a, g, g - gb, lane, lane_lt, w, dl[u], ring, cring, ring6, ch, acc);
         }
       }
     }
     // chunk epilogue: the partial last record block, then one store per bitmap for the chunk
 #ifndef RTN_EXP_NO_STORES
     rtn_wave_sync();
-    rtn_flush(a, ring, ch, lane, ch.nrec - ch.nflushed);
+    rtn_flush(a, ring, cring, ch, lane, ch.nrec - ch.nflushed);
     if (stage6) rtn_flush6(a, ring6, ch, lane, ch.nv6 - ch.nv6flushed);
     rtn_wave_sync();
 #endif
