@@ -168,6 +168,14 @@ def e2e_rate(ctx, slab: np.ndarray, dlen: np.ndarray, stride: int, dev) -> dict:
                     "2 streams; PCIe-bound"}
 
 
+def counters_fwd_hint(out) -> int:
+    """Forwarded frames of a finished run (popcount of its fwd bitmap)."""
+    import numpy as np_
+
+    bm = out.fwd_bitmap.cpu().numpy().view(np_.uint8)
+    return int(np_.unpackbits(bm).sum())
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -265,9 +273,27 @@ def main() -> None:
         c1.record(stream)
         torch.cuda.synchronize(dev)
         cms = c0.elapsed_time(c1) / args.steps
+        # connection lookup (include/retina_ct.h) over the same batch: insert + lookup launches on a
+        # 2^24-slot (1 GiB) table; the first pass opens every SYN-only/UDP flow, the timed passes
+        # then find them (Occupied) and drop the rest (Vacant, not an opener)
+        ct = pc.ConnTable(local, 24)
+        ct_out = ct.process(cout, stream=stream)
+        k0 = torch.cuda.Event(enable_timing=True)
+        k1 = torch.cuda.Event(enable_timing=True)
+        k0.record(stream)
+        for _ in range(args.steps):
+            ct.process(cout, out=ct_out, stream=stream)
+        k1.record(stream)
+        torch.cuda.synchronize(dev)
+        ctms = k0.elapsed_time(k1) / args.steps
+        ct_stats = ct.stats()
+        del ct
         conn_stage = {"kernel_ms": round(cms, 4), "mpps": round(n / cms / 1e3, 1),
                       "vs_filter_only": round(kern_ms / cms, 3),
                       "first_packet_tree_size": prog.info["conn_tree_size"],
+                      "ct_lookup": {"ms": round(ctms, 4), "mpps": round(n / ctms / 1e3, 1),
+                                    "forwarded_per_s_M": round(counters_fwd_hint(cout) / ctms / 1e3, 1),
+                                    "table_slots": ct_stats["capacity"], "live": ct_stats["live"]},
                       "note": "same step + rtn_conn_t (8 B) per forwarded frame: ConnId hash/orientation, "
                               "creates bit, first-packet packet_filter actions"}
         del cout

@@ -190,3 +190,66 @@ def stage(pf: PacketFilter, frame: bytes, dl: int) -> tuple[int, int, list[int]]
 
 
 __all__ = ["PacketFilter", "stage", "conn_hash", "conn_id", "creates", "Hdr", "be"]
+
+
+# ----------------------------------------------------------------------------------------------
+# The table step of ConnTracker::process (conntrack/mod.rs:80-169), batch by batch.
+
+CT_HIT, CT_NEW, CT_MISS, CT_NEW_DROPPED, CT_FULL, CT_COLLISION, CT_PRIOR = 1, 2, 3, 4, 5, 6, 0x100
+
+
+def conn_key(ctx) -> tuple:
+    """The canonical ConnId of a forwarded frame's L4Context (direction-free)."""
+    _, mx, mn = conn_id(ctx)
+    return (ctx.ver, mx, mn, ctx.proto)
+
+
+class TableModel:
+    """Sequential restatement of the table outcome of every forwarded frame, in frame order.
+
+    Within a batch an existing connection is assumed to stay (the host sees its own removals and
+    reports them with remove() between batches). A frame finds its key Occupied (HIT), or, on a
+    Vacant key, opens the connection if it may (Conn::new_tcp: SYN without ACK/RST; Conn::new_udp:
+    any UDP frame) unless it is a TCP frame whose first-packet filter drops (remove_from_table
+    right after filter_first_packet: no entry, mod.rs:139-141), else it is dropped (MISS).
+    Slots are opaque here: the model hands out ids; tests compare the GPU's slot *partition*."""
+
+    def __init__(self, max_connections: int = 1 << 62):
+        self.present: dict = {}   # key -> (model id, epoch inserted)
+        self.max = max_connections
+        self.epoch = 0
+        self._ids = 0
+
+    def process(self, frames: list[tuple]) -> list[tuple]:
+        """frames: (key, opens, pf_drops) per forwarded frame in frame order.
+        Returns (model id or None, status) per frame."""
+        self.epoch += 1
+        first: dict = {}
+        for i, (key, opens, drops) in enumerate(frames):
+            inserting = opens and not (key[3] == 6 and drops)
+            if inserting and key not in self.present and key not in first:
+                first[key] = i
+        for key, i in sorted(first.items(), key=lambda kv: kv[1]):
+            if len(self.present) < self.max:
+                self.present[key] = (self._ids, self.epoch)
+                self._ids += 1
+        out = []
+        for i, (key, opens, drops) in enumerate(frames):
+            dropped_opener = opens and key[3] == 6 and drops
+            if key in self.present:
+                mid, ep = self.present[key]
+                if ep != self.epoch:
+                    out.append((mid, CT_HIT | CT_PRIOR))
+                elif i > first[key]:
+                    out.append((mid, CT_HIT))
+                elif i == first[key]:
+                    out.append((mid, CT_NEW))
+                else:
+                    out.append((mid, CT_NEW_DROPPED if opens else CT_MISS))
+            else:
+                out.append((None, CT_MISS if not opens else CT_NEW_DROPPED if dropped_opener else CT_FULL))
+        return out
+
+    def remove(self, keys) -> None:
+        for k in keys:
+            self.present.pop(k, None)

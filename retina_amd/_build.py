@@ -33,13 +33,14 @@ def _stale(target: Path, deps: list[Path]) -> bool:
     return any(d.stat().st_mtime > t for d in deps)
 
 
-def _gen_kernel_inc() -> Path:
-    src = CSRC / "kernels" / "pc_kernel.hip"
-    inc = CSRC / "runtime" / "pc_kernel_src.inc"
+def _gen_kernel_inc(name: str = "pc_kernel", var: str = "kPcKernelSrc") -> Path:
+    """Embed a kernel source as a C++ raw string (compiled by hiprtc at run time)."""
+    src = CSRC / "kernels" / f"{name}.hip"
+    inc = CSRC / "runtime" / f"{name}_src.inc"
     text = src.read_text()
     delim = "RTNSRC"
     assert f"){delim}\"" not in text
-    body = f'static const char* const kPcKernelSrc = R"{delim}(' + text + f'){delim}";\n'
+    body = f'static const char* const {var} = R"{delim}(' + text + f'){delim}";\n'
     if not inc.exists() or inc.read_text() != body:
         inc.write_text(body)
     return inc
@@ -48,10 +49,11 @@ def _gen_kernel_inc() -> Path:
 def build_library(force: bool = False) -> Path:
     LIB.mkdir(exist_ok=True)
     inc = _gen_kernel_inc()
+    inc_ct = _gen_kernel_inc("ct_kernel", "kCtKernelSrc")
     fg = [CSRC / "filtergen" / s for s in FILTERGEN_SRCS]
     rt = [CSRC / "runtime" / "rtn_runtime.cpp", CSRC / "ingest" / "pcap_ingest.cpp"]
     hdrs = (list((CSRC / "filtergen").glob("*.hpp")) + list((CSRC / "runtime").glob("*.hpp"))
-            + list((ROOT / "include").glob("*.h")) + [inc])
+            + list((ROOT / "include").glob("*.h")) + [inc, inc_ct])
     so = LIB / SO_NAME
     if force or _stale(so, fg + rt + hdrs):
         cmd = [

@@ -1,6 +1,7 @@
 // C-ABI runtime: compile subscription specs, build the specialised gfx950 kernel with hiprtc,
 // load it and launch it. See include/retina_pc.h for the contract and reference map.
 #include "retina_pc.h"
+#include "retina_ct.h"
 
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
@@ -28,6 +29,7 @@ int32_t rtn::set_error(int32_t code, const std::string& msg) {
 namespace {
 
 #include "pc_kernel_src.inc"  // kPcKernelSrc: csrc/kernels/pc_kernel.hip as a string literal
+#include "ct_kernel_src.inc"  // kCtKernelSrc: csrc/kernels/ct_kernel.hip
 
 int32_t fail(int32_t code, const std::string& msg) { return rtn::set_error(code, msg); }
 
@@ -417,5 +419,169 @@ size_t rtn_out_dlv_bytes(uint32_t n, uint32_t deliver_words) {
 static_assert(sizeof(rtn_conn_t) == 8, "rtn_conn_t is 8 bytes");
 size_t rtn_out_conn_bytes(uint32_t n) { return chunked(n) * sizeof(rtn_conn_t); }
 size_t rtn_out_conn_dlv_bytes(uint32_t n, uint32_t conn_words) { return chunked(n) * conn_words * 8u; }
+
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------------------------
+// Connection lookup (include/retina_ct.h)
+
+struct rtn_ct {
+  int device = 0;
+  uint32_t cap = 0, max_live = 0, epoch = 0;
+  uint32_t* table = nullptr;
+  uint32_t* live = nullptr;  // [0] live slots
+  hipModule_t module = nullptr;
+  hipFunction_t insert = nullptr, lookup = nullptr, remove = nullptr, clear = nullptr, rehash = nullptr;
+};
+
+namespace {
+struct CtArgs {  // must match struct rtn_ct_args in ct_kernel.hip
+  const uint64_t* fwd_bm;
+  const uint32_t* recs;
+  const uint32_t* addr6;
+  const uint64_t* conn;
+  uint64_t* out;
+  uint32_t* table;
+  uint32_t* live;
+  uint32_t n;
+  uint32_t cap_mask;
+  uint32_t max_live;
+  uint32_t epoch;
+};
+
+int32_t hip_fail(const char* what, hipError_t e) { return fail(RTN_EDEVICE, std::string(what) + ": " + hipGetErrorString(e)); }
+
+int32_t ct_clear(rtn_ct* ct, uint32_t* table, hipStream_t s) {
+  uint32_t cap = ct->cap;
+  void* p[] = {&table, &cap};
+  hipError_t e = hipModuleLaunchKernel(ct->clear, (cap + 255u) / 256u, 1, 1, 256, 1, 1, 0, s, p, nullptr);
+  return e == hipSuccess ? RTN_OK : hip_fail("rtn_ct_clear", e);
+}
+}  // namespace
+
+extern "C" {
+
+int32_t rtn_ct_create(int device, uint32_t capacity_log2, uint32_t max_connections, rtn_ct_t** out) {
+  if (!out) return fail(RTN_EINVAL, "null argument");
+  if (capacity_log2 < 6 || capacity_log2 > 30) return fail(RTN_EINVAL, "capacity_log2 must be in [6, 30]");
+  std::shared_ptr<std::vector<uint8_t>> code;
+  int32_t rc = compile_code_object(kCtKernelSrc, code);
+  if (rc) return rc;
+  auto ct = std::make_unique<rtn_ct>();
+  ct->device = device;
+  ct->cap = 1u << capacity_log2;
+  ct->max_live = max_connections;
+  if (hipSetDevice(device) != hipSuccess) return fail(RTN_EDEVICE, "hipSetDevice failed");
+  hipError_t e = hipModuleLoadData(&ct->module, code->data());
+  if (e != hipSuccess) return hip_fail("hipModuleLoadData", e);
+  const char* names[] = {"rtn_ct_insert", "rtn_ct_lookup", "rtn_ct_remove_k", "rtn_ct_clear", "rtn_ct_rehash"};
+  hipFunction_t* fns[] = {&ct->insert, &ct->lookup, &ct->remove, &ct->clear, &ct->rehash};
+  for (int k = 0; k < 5; ++k) {
+    e = hipModuleGetFunction(fns[k], ct->module, names[k]);
+    if (e != hipSuccess) return hip_fail("hipModuleGetFunction", e);
+  }
+  e = hipMalloc(reinterpret_cast<void**>(&ct->table), (size_t)ct->cap * 64u);
+  if (e != hipSuccess) return hip_fail("hipMalloc(table)", e);
+  e = hipMalloc(reinterpret_cast<void**>(&ct->live), 16);
+  if (e != hipSuccess) return hip_fail("hipMalloc", e);
+  e = hipMemset(ct->live, 0, 16);
+  if (e != hipSuccess) return hip_fail("hipMemset", e);
+  rc = ct_clear(ct.get(), ct->table, nullptr);
+  if (rc) return rc;
+  e = hipDeviceSynchronize();
+  if (e != hipSuccess) return hip_fail("hipDeviceSynchronize", e);
+  *out = ct.release();
+  return RTN_OK;
+}
+
+int32_t rtn_ct_destroy(rtn_ct_t* ct) {
+  if (!ct) return RTN_OK;
+  if (ct->table) (void)hipFree(ct->table);
+  if (ct->live) (void)hipFree(ct->live);
+  if (ct->module) (void)hipModuleUnload(ct->module);
+  delete ct;
+  return RTN_OK;
+}
+
+int32_t rtn_ct_process(rtn_ct_t* ct, const rtn_pc_out_t* pc, uint32_t n, rtn_ct_entry_t* out, void* stream) {
+  if (!ct || !pc || !out) return fail(RTN_EINVAL, "null argument");
+  if (n == 0) return RTN_OK;
+  if (!pc->fwd_bitmap || !pc->l4 || !pc->conn) return fail(RTN_EINVAL, "rtn_pc_out_t needs fwd_bitmap, l4 and conn");
+  if (!pc->addr6) return fail(RTN_EINVAL, "rtn_pc_out_t needs addr6 (IPv6 keys)");
+  CtArgs a;
+  a.fwd_bm = pc->fwd_bitmap;
+  a.recs = reinterpret_cast<const uint32_t*>(pc->l4);
+  a.addr6 = reinterpret_cast<const uint32_t*>(pc->addr6);
+  a.conn = reinterpret_cast<const uint64_t*>(pc->conn);
+  a.out = reinterpret_cast<uint64_t*>(out);
+  a.table = ct->table;
+  a.live = ct->live;
+  a.n = n;
+  a.cap_mask = ct->cap - 1u;
+  a.max_live = ct->max_live;
+  a.epoch = ++ct->epoch;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const uint32_t chunks = (n + RTN_CHUNK_FRAMES - 1u) / RTN_CHUNK_FRAMES;
+  const uint32_t blocks = (chunks + 3u) / 4u;  // one wave per chunk
+  void* p[] = {&a};
+  hipError_t e = hipModuleLaunchKernel(ct->insert, blocks, 1, 1, 256, 1, 1, 0, s, p, nullptr);
+  if (e != hipSuccess) return hip_fail("rtn_ct_insert", e);
+  e = hipModuleLaunchKernel(ct->lookup, blocks, 1, 1, 256, 1, 1, 0, s, p, nullptr);
+  if (e != hipSuccess) return hip_fail("rtn_ct_lookup", e);
+  return RTN_OK;
+}
+
+int32_t rtn_ct_remove(rtn_ct_t* ct, const uint32_t* slots, uint32_t n, void* stream) {
+  if (!ct || (!slots && n)) return fail(RTN_EINVAL, "null argument");
+  if (n == 0) return RTN_OK;
+  uint32_t mask = ct->cap - 1u;
+  uint32_t* table = ct->table;
+  uint32_t* live = ct->live;
+  void* p[] = {&table, &live, &slots, &n, &mask};
+  hipError_t e = hipModuleLaunchKernel(ct->remove, (n + 255u) / 256u, 1, 1, 256, 1, 1, 0,
+                                       reinterpret_cast<hipStream_t>(stream), p, nullptr);
+  return e == hipSuccess ? RTN_OK : hip_fail("rtn_ct_remove", e);
+}
+
+int32_t rtn_ct_rebuild(rtn_ct_t* ct, uint32_t* new_slot, void* stream) {
+  if (!ct || !new_slot) return fail(RTN_EINVAL, "null argument");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  uint32_t* dst = nullptr;
+  hipError_t e = hipMalloc(reinterpret_cast<void**>(&dst), (size_t)ct->cap * 64u);
+  if (e != hipSuccess) return hip_fail("hipMalloc(rebuild)", e);
+  int32_t rc = ct_clear(ct, dst, s);
+  if (rc) {
+    (void)hipFree(dst);
+    return rc;
+  }
+  const uint32_t* src = ct->table;
+  uint32_t mask = ct->cap - 1u;
+  void* p[] = {&src, &dst, &new_slot, &mask};
+  e = hipModuleLaunchKernel(ct->rehash, (ct->cap + 255u) / 256u, 1, 1, 256, 1, 1, 0, s, p, nullptr);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) {
+    (void)hipFree(dst);
+    return hip_fail("rtn_ct_rehash", e);
+  }
+  (void)hipFree(ct->table);
+  ct->table = dst;
+  return RTN_OK;
+}
+
+int32_t rtn_ct_stats(rtn_ct_t* ct, rtn_ct_stats_t* st) {
+  if (!ct || !st) return fail(RTN_EINVAL, "null argument");
+  uint32_t live = 0;
+  hipError_t e = hipMemcpy(&live, ct->live, 4, hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return hip_fail("hipMemcpy", e);
+  st->capacity = ct->cap;
+  st->live = live;
+  st->epoch = ct->epoch;
+  st->max_connections = ct->max_live;
+  return RTN_OK;
+}
+
+void* rtn_ct_table(rtn_ct_t* ct) { return ct ? ct->table : nullptr; }
+size_t rtn_out_ct_bytes(uint32_t n) { return chunked(n) * sizeof(rtn_ct_entry_t); }
 
 }  // extern "C"

@@ -75,6 +75,15 @@ EXPORTS = {
     "rtn_out_dlv_bytes": (C.c_size_t, [C.c_uint32, C.c_uint32]),
     "rtn_out_conn_bytes": (C.c_size_t, [C.c_uint32]),
     "rtn_out_conn_dlv_bytes": (C.c_size_t, [C.c_uint32, C.c_uint32]),
+    # include/retina_ct.h
+    "rtn_ct_create": (C.c_int32, [C.c_int, C.c_uint32, C.c_uint32, C.POINTER(C.c_void_p)]),
+    "rtn_ct_destroy": (C.c_int32, [C.c_void_p]),
+    "rtn_ct_process": (C.c_int32, [C.c_void_p, C.POINTER(_Out), C.c_uint32, C.c_void_p, C.c_void_p]),
+    "rtn_ct_remove": (C.c_int32, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p]),
+    "rtn_ct_rebuild": (C.c_int32, [C.c_void_p, C.c_void_p, C.c_void_p]),
+    "rtn_ct_stats": (C.c_int32, [C.c_void_p, C.c_void_p]),
+    "rtn_ct_table": (C.c_void_p, [C.c_void_p]),
+    "rtn_out_ct_bytes": (C.c_size_t, [C.c_uint32]),
     # include/retina_ingest.h
     "rtn_pcap_open": (C.c_int32, [C.c_char_p, C.c_uint32, C.POINTER(C.c_void_p)]),
     "rtn_pcap_next_batch": (C.c_int32, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint32,
@@ -350,13 +359,87 @@ class PacketContinue:
             out = self.alloc_outputs(n)
         b = _Batch(slab.data_ptr(), stride, data_len.data_ptr(), n, core_id,
                    ext.data_ptr() if ext is not None else None)
-        ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
-        o = _Out(ptr(out.pc_bitmap), ptr(out.fwd_bitmap), ptr(out.l4), ptr(out.addr6), ptr(out.dlv_bitmap),
-                 ptr(out.dlv_records), ptr(out.counters), ptr(out.conn), ptr(out.conn_dlv))
+        o = _out_struct(out)
         s = stream if stream is not None else torch.cuda.current_stream(self.device)
         _check(lib().rtn_pc_run(self._h, C.byref(b), C.byref(o), C.c_void_p(s.cuda_stream)))
         out.n = n
         return out
+
+
+def _out_struct(out: PCOutputs) -> _Out:
+    ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
+    return _Out(ptr(out.pc_bitmap), ptr(out.fwd_bitmap), ptr(out.l4), ptr(out.addr6), ptr(out.dlv_bitmap),
+                ptr(out.dlv_records), ptr(out.counters), ptr(out.conn), ptr(out.conn_dlv))
+
+
+class _CtStats(C.Structure):
+    _fields_ = [("capacity", C.c_uint32), ("live", C.c_uint32), ("epoch", C.c_uint32),
+                ("max_connections", C.c_uint32)]
+
+
+CT_HIT, CT_NEW, CT_MISS, CT_NEW_DROPPED, CT_FULL, CT_COLLISION, CT_PRIOR = 1, 2, 3, 4, 5, 6, 0x100
+CT_NO_SLOT = 0xFFFFFFFF
+
+
+class ConnTable:
+    """GPU connection lookup (include/retina_ct.h): the ConnTracker table step for whole batches,
+    on a table resident in HBM. process() takes the PCOutputs of rtn_pc_run (with conn=True)."""
+
+    def __init__(self, device: int = 0, capacity_log2: int = 20, max_connections: int | None = None):
+        self.device = device
+        h = C.c_void_p()
+        cap = 1 << capacity_log2
+        _check(lib().rtn_ct_create(device, capacity_log2, max_connections if max_connections is not None else cap,
+                                   C.byref(h)))
+        self._h = h
+        self.capacity = cap
+
+    def __del__(self):
+        if getattr(self, "_h", None) and self._h.value and _lib is not None:
+            _lib.rtn_ct_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def process(self, pc_out: PCOutputs, out=None, stream=None):
+        """Returns a device uint8 tensor of rtn_ct_entry_t (slot, status) indexed like pc_out.l4."""
+        import torch
+
+        if pc_out.conn is None or pc_out.addr6 is None:
+            raise RetinaError(-22, "ConnTable.process needs outputs allocated with conn=True and addr6=True")
+        n = pc_out.n
+        if out is None:
+            out = torch.empty(lib().rtn_out_ct_bytes(max(n, 1)), dtype=torch.uint8, device=torch.device("cuda", self.device))
+        o = _out_struct(pc_out)
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        _check(lib().rtn_ct_process(self._h, C.byref(o), n, C.c_void_p(out.data_ptr()), C.c_void_p(s.cuda_stream)))
+        return out
+
+    def remove(self, slots, stream=None) -> None:
+        """slots: device int32/uint32 tensor of connection handles."""
+        import torch
+
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        _check(lib().rtn_ct_remove(self._h, C.c_void_p(slots.data_ptr()), int(slots.numel()), C.c_void_p(s.cuda_stream)))
+
+    def rebuild(self, stream=None):
+        """Compact tombstones; returns the device old-slot -> new-slot map (uint32 view in int32)."""
+        import torch
+
+        m = torch.empty(self.capacity, dtype=torch.int32, device=torch.device("cuda", self.device))
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        _check(lib().rtn_ct_rebuild(self._h, C.c_void_p(m.data_ptr()), C.c_void_p(s.cuda_stream)))
+        return m
+
+    def stats(self) -> dict:
+        st = _CtStats()
+        _check(lib().rtn_ct_stats(self._h, C.byref(st)))
+        return {f: getattr(st, f) for f, _ in _CtStats._fields_}
+
+
+def decode_ct(entries, pc_out: PCOutputs) -> np.ndarray:
+    """rtn_ct_entry_t of the forwarded frames in frame order: (slot, status) uint32 pairs."""
+    fwd_bm = pc_out.fwd_bitmap.cpu().numpy().view(np.uint64)
+    e = entries.cpu().numpy().view(np.uint32).reshape(-1, 2)
+    return e[_segment_index(fwd_bm)]
 
 
 def split_slab(slab: np.ndarray, stride: int) -> tuple[np.ndarray, np.ndarray]:

@@ -125,3 +125,54 @@ def assert_same(gpu: dict, ora: dict, what: str = "") -> None:
         c = gpu["counters"]
         assert c[0] == ora["pc"].sum() and c[1] == ora["fwd"].sum(), f"{what}: counters {c}"
         assert c[2] == int((ora["dm"] != 0).any(1).sum()) if ora["dm"].size else c[2] == 0
+
+
+def build_frame(v6=False, src=0x0A000001, dst=0x0A000002, sport=1234, dport=80, proto=6, flags=0x02,
+                payload=b"") -> bytes:
+    """One Eth/IPv4|IPv6/TCP|UDP frame with the given 5-tuple and TCP flags."""
+    import struct
+
+    if proto == 6:
+        l4 = struct.pack(">HHIIBBHHH", sport, dport, 1, 2, 0x50, flags, 1024, 0, 0) + payload
+    else:
+        l4 = struct.pack(">HHHH", sport, dport, 8 + len(payload), 0) + payload
+    if v6:
+        ip = struct.pack(">IHBB", 0x60000000, len(l4), proto, 64) + src.to_bytes(16, "big") + dst.to_bytes(16, "big")
+        et = 0x86DD
+    else:
+        ip = struct.pack(">BBHHHBBHII", 0x45, 0, 20 + len(l4), 0, 0, 64, proto, 0, src, dst)
+        et = 0x0800
+    return bytes(6) + bytes(5) + b"\x01" + struct.pack(">H", et) + ip + l4
+
+
+def flow_pool(rng: np.random.Generator, nflows: int) -> list[tuple]:
+    """Distinct connections: (v6, ip_a, ip_b, port_a, port_b, proto)."""
+    pool, seen = [], set()
+    while len(pool) < nflows:
+        v6 = bool(rng.random() < 0.3)
+        bits = 128 if v6 else 32
+        a = int(rng.integers(0, 1 << 62)) << (bits - 62) if v6 else int(rng.integers(0, 1 << 32))
+        b = int(rng.integers(0, 1 << 62)) << (bits - 62) if v6 else int(rng.integers(0, 1 << 32))
+        pa, pb = int(rng.integers(1, 65536)), int(rng.integers(1, 65536))
+        if rng.random() < 0.05:        # equal addresses: the port decides the orientation
+            b = a
+        proto = 6 if rng.random() < 0.7 else 17
+        k = (v6, a, b, pa, pb, proto)
+        if k not in seen:
+            seen.add(k)
+            pool.append(k)
+    return pool
+
+
+def flow_frames(rng: np.random.Generator, pool: list[tuple], n: int, p_syn: float = 0.3) -> list[bytes]:
+    """n frames drawn from the flows of `pool`, random direction, TCP flags SYN-only with p_syn,
+    otherwise a random mix (ACK, SYN|ACK, RST, FIN|ACK, PSH|ACK)."""
+    frames = []
+    other = [0x10, 0x12, 0x04, 0x11, 0x18, 0x06]
+    for _ in range(n):
+        v6, a, b, pa, pb, proto = pool[int(rng.integers(0, len(pool)))]
+        if rng.random() < 0.5:
+            a, b, pa, pb = b, a, pb, pa
+        fl = 0x02 if rng.random() < p_syn else other[int(rng.integers(0, len(other)))]
+        frames.append(build_frame(v6, a, b, pa, pb, proto, fl))
+    return frames

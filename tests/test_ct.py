@@ -1,0 +1,158 @@
+"""GPU connection lookup (include/retina_ct.h) against the sequential table model
+(oracle/conn.py TableModel): per-frame Occupied/Vacant outcome in frame order, the admission
+rules, removals between batches, capacity, and rebuild. Slot numbers depend on probe races, so
+the GPU's slots are compared as a partition: one slot per connection, stable across batches."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+import helpers
+from golden.filter_sets import SETS
+from oracle import conn as oconn
+from oracle import packet
+from retina_amd import pc
+
+SPEC = SETS["port_count"]  # every TCP/UDP frame is forwarded; first-packet actions never drop
+
+
+def _model_frames(frames: list[bytes], pf: oconn.PacketFilter):
+    out = []
+    for f in frames:
+        ctx = packet.l4context(f + bytes(64), len(f))
+        assert ctx is not None
+        data, term, _ = pf.evaluate(f, len(f))
+        out.append((oconn.conn_key(ctx), oconn.creates(ctx), data == 0 and term == 0))
+    return out
+
+
+def test_model_admission_rules():
+    m = oconn.TableModel()
+    k = (4, (2, 80), (1, 5000), 6)
+    u = (4, (2, 53), (1, 6000), 17)
+    st = m.process([(k, False, False), (k, True, True), (k, True, False), (k, False, False), (u, True, True)])
+    assert [s for _, s in st] == [oconn.CT_MISS, oconn.CT_NEW_DROPPED, oconn.CT_NEW, oconn.CT_HIT, oconn.CT_NEW]
+    st = m.process([(k, False, False), (u, False, False)])
+    assert [s for _, s in st] == [oconn.CT_HIT | oconn.CT_PRIOR] * 2
+    m.remove([k])
+    assert [s for _, s in m.process([(k, False, False)])] == [oconn.CT_MISS]
+    small = oconn.TableModel(max_connections=1)
+    st = small.process([(k, True, False), (u, True, False)])
+    assert [s for _, s in st] == [oconn.CT_NEW, oconn.CT_FULL]
+
+
+class _Run:
+    def __init__(self, cap_log2=16, max_conn=None):
+        import torch
+
+        self.torch = torch
+        self.prog = pc.Program.from_spec(SPEC)
+        self.ctx = pc.PacketContinue(self.prog, 0)
+        self.ct = pc.ConnTable(0, cap_log2, max_conn)
+        self.pf = oconn.PacketFilter(self.prog.tree_json(1), helpers.subs_from_spec(SPEC))
+
+    def batch(self, frames):
+        torch = self.torch
+        slab, dlen = pc.pack_frames(frames, 128)
+        dev = torch.device("cuda", 0)
+        out = self.ctx.alloc_outputs(len(frames), conn=True)
+        self.ctx.run(torch.from_numpy(slab).to(dev), 128, torch.from_numpy(dlen.view(np.int16)).to(dev),
+                     len(frames), out)
+        ent = self.ct.process(out)
+        torch.cuda.synchronize()
+        fwd = out.decode()["fwd"]
+        assert fwd.all()
+        return pc.decode_ct(ent, out)
+
+
+def _check(got: np.ndarray, exp: list, ids: dict, owner: dict) -> None:
+    """Statuses equal; the GPU slot of each model connection is one fixed slot (ids), never shared
+    by two live connections (owner)."""
+    st = got[:, 1]
+    want = np.array([s for _, s in exp], np.uint32)
+    bad = np.nonzero(st != want)[0]
+    assert bad.size == 0, f"status differs at frames {bad[:8]}: {st[bad[:8]]} vs {want[bad[:8]]}"
+    for (mid, _), slot in zip(exp, got[:, 0]):
+        if mid is None:
+            assert slot == pc.CT_NO_SLOT
+            continue
+        assert slot != pc.CT_NO_SLOT
+        if mid in ids:
+            assert ids[mid] == slot, f"connection {mid} moved from slot {ids[mid]} to {slot}"
+        else:
+            assert owner.get(int(slot)) is None, f"slot {slot} already holds connection {owner.get(int(slot))}"
+            ids[mid] = int(slot)
+            owner[int(slot)] = mid
+
+
+@pytest.mark.gpu
+def test_ct_batches_vs_model(gpu):
+    rng = np.random.default_rng(7)
+    pool = helpers.flow_pool(rng, 1500)
+    r = _Run()
+    model = oconn.TableModel()
+    ids, owner = {}, {}
+    for b in range(4):
+        frames = helpers.flow_frames(rng, pool, 6000 + 37 * b)
+        exp = model.process(_model_frames(frames, r.pf))
+        got = r.batch(frames)
+        _check(got, exp, ids, owner)
+        # the host decides to remove ~20% of the live connections (terminated / expired)
+        live = list(model.present.items())
+        drop = [live[i] for i in rng.choice(len(live), size=len(live) // 5, replace=False)]
+        slots = np.array([ids[mid] for _, (mid, _) in drop], np.uint32)
+        r.ct.remove(r.torch.from_numpy(slots.view(np.int32)).to("cuda:0"))
+        model.remove([k for k, _ in drop])
+        for _, (mid, _) in drop:
+            owner.pop(ids.pop(mid), None)
+    st = r.ct.stats()
+    assert st["live"] == len(model.present) and st["epoch"] == 4
+
+
+@pytest.mark.gpu
+def test_ct_capacity(gpu):
+    rng = np.random.default_rng(11)
+    pool = helpers.flow_pool(rng, 400)
+    r = _Run(cap_log2=12, max_conn=64)
+    frames = helpers.flow_frames(rng, pool, 3000, p_syn=0.5)
+    mf = _model_frames(frames, r.pf)
+    got = r.batch(frames)
+    assert r.ct.stats()["live"] == 64
+    # which 64 connections get in is not frame-ordered on the GPU; every connection's frames agree
+    by_key: dict = {}
+    for (key, opens, _), (slot, status) in zip(mf, got):
+        by_key.setdefault(key, []).append((int(slot), int(status), opens))
+    admitted = 0
+    for key, fr in by_key.items():
+        slots = {s for s, _, _ in fr}
+        if slots == {pc.CT_NO_SLOT}:
+            assert all(st == (pc.CT_FULL if o else pc.CT_MISS) for _, st, o in fr)
+        else:
+            admitted += 1
+            assert len(slots - {pc.CT_NO_SLOT}) == 1
+            assert sum(st == pc.CT_NEW for _, st, _ in fr) == 1
+    assert admitted == 64
+
+
+@pytest.mark.gpu
+def test_ct_rebuild_moves_connections(gpu):
+    rng = np.random.default_rng(5)
+    pool = helpers.flow_pool(rng, 800)
+    r = _Run(cap_log2=12)
+    model = oconn.TableModel()
+    ids, owner = {}, {}
+    frames = helpers.flow_frames(rng, pool, 4000, p_syn=0.6)
+    _check(r.batch(frames), model.process(_model_frames(frames, r.pf)), ids, owner)
+    live = list(model.present.items())
+    drop = live[::2]
+    r.ct.remove(r.torch.from_numpy(np.array([ids[m] for _, (m, _) in drop], np.uint32).view(np.int32)).to("cuda:0"))
+    model.remove([k for k, _ in drop])
+    for _, (m, _) in drop:
+        owner.pop(ids.pop(m), None)
+    new_slot = r.ct.rebuild().cpu().numpy().view(np.uint32)
+    ids = {m: int(new_slot[s]) for m, s in ids.items()}
+    assert all(s != pc.CT_NO_SLOT for s in ids.values())
+    owner = {s: m for m, s in ids.items()}
+    frames = helpers.flow_frames(rng, pool, 4000, p_syn=0.2)
+    _check(r.batch(frames), model.process(_model_frames(frames, r.pf)), ids, owner)
+    assert r.ct.stats()["live"] == len(model.present)
