@@ -59,7 +59,10 @@ typedef struct rtn_ct_stats {
 } rtn_ct_stats_t;
 
 /* A table of 2^capacity_log2 64-byte slots on `device`, admitting at most max_connections
- * (ConnTrackConfig::max_connections). Keep the load factor below ~0.5 for short probe chains. */
+ * (ConnTrackConfig::max_connections). Keep the load factor below ~0.5 for short probe chains.
+ * When a batch fills the table, which openers get the last slots is not frame-ordered, and
+ * duplicate openers racing for one key can hold a reservation briefly, so such a batch may
+ * admit a few fewer than max_connections. */
 int32_t rtn_ct_create(int device, uint32_t capacity_log2, uint32_t max_connections, rtn_ct_t** out);
 int32_t rtn_ct_destroy(rtn_ct_t* ct);
 /* One batch (n frames, the same batch rtn_pc_run processed into `pc`): two launches on `stream`.

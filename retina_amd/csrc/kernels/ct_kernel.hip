@@ -9,6 +9,10 @@
 //   [16] u32 key[10]  max ip (4 words; IPv4 in word 0), min ip, max port << 16 | min port,
 //                     proto | 0x100 for IPv6: ConnId (conntrack/conn_id.rs:115-117)
 //
+// Occupancy bitmap: one bit per slot, set when a slot is claimed and cleared only by a rebuild
+// (2 MiB for 2^24 slots: it stays in each XCD's 4-MiB L2). A probe whose start slot has a clear
+// bit is a miss without touching the table, which is what most frames of a busy link are.
+//
 // Two launches per batch, so every frame sees the same table state:
 //   rtn_ct_insert  frames that open a connection on a miss (rtn_conn_t creates bit; a TCP opener
 //                  whose first-packet filter drops is not inserted: remove_from_table after
@@ -16,8 +20,8 @@
 //                  (CAS on the tag), then lower the slot's `first` to their frame index.
 //   rtn_ct_lookup  every forwarded frame finds its key (tags, then the whole key, so a 64-bit
 //                  fingerprint collision is reported instead of aliasing) and gets its status.
-// A wave walks one 512-frame chunk: lane = frame, records ranked by the fwd bitmap exactly as
-// rtn_pc_run wrote them.
+// A block walks one 512-frame chunk, a wave one group: lane = frame, records ranked by the fwd
+// bitmap exactly as rtn_pc_run wrote them.
 #ifndef __HIPCC_RTC__
 #include <hip/hip_runtime.h>
 #endif
@@ -46,11 +50,13 @@ struct rtn_ct_args {
   const rtn_u64* conn;        // rtn_conn_t
   rtn_u64* out;               // rtn_ct_entry_t (slot | status << 32), indexed like recs
   rtn_u32* table;             // cap * 16 words
-  rtn_u32* live;              // [0] live slots, [1] batch epoch
+  rtn_u32* occ;               // cap bits: slot not empty (live or removed); small enough for L2
+  rtn_u32* live;              // [64] live-slot counters (their sum); [0] alone in checked mode
   rtn_u32 n;                  // frames in the batch
   rtn_u32 cap_mask;
   rtn_u32 max_live;
   rtn_u32 epoch;
+  rtn_u32 check;              // 1: admit against max_live (host folded the counters into [0])
 };
 
 struct rtn_ct_key {
@@ -78,11 +84,11 @@ __device__ __forceinline__ rtn_u32 rtn_ct_fmix(rtn_u32 h) {
   return h ^ (h >> 16);
 }
 
-// Canonical key of record r (v6r: its rank among the chunk's IPv6 records) + its 64-bit fingerprint.
-__device__ __forceinline__ void rtn_ct_make_key(const rtn_ct_args& a, rtn_u64 r, rtn_u64 v6r, rtn_ct_key& k) {
-  const rtn_u32* rec = a.recs + r * 6u;
+// Canonical key of a record (its 6 words, its rtn_conn_t, its IPv6 addresses or null) + its
+// 64-bit fingerprint.
+__device__ __forceinline__ void rtn_ct_make_key(const rtn_ct_args& a, const rtn_u32 (&rec)[6], rtn_u64 c,
+                                                const rtn_u32* a6, rtn_ct_key& k) {
   const rtn_u32 meta = rec[5];
-  const rtn_u64 c = a.conn[r];
   k.h = (rtn_u32)c;
   k.info = (rtn_u32)(c >> 32);
   k.v6 = (meta >> 7) & 1u;
@@ -90,12 +96,9 @@ __device__ __forceinline__ void rtn_ct_make_key(const rtn_ct_args& a, rtn_u64 r,
   const bool gt = (k.info >> 27) & 1u;  // src is the max endpoint
   rtn_u32 s[4], d[4];
   if (k.v6) {
-    const rtn_u32* a6 = a.addr6 + v6r * 8u;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      s[j] = __builtin_bswap32(a6[j]);      // raw bytes -> big-endian words, most significant first
-      d[j] = __builtin_bswap32(a6[4 + j]);
-    }
+    const uint4 x = reinterpret_cast<const uint4*>(a6)[0], y = reinterpret_cast<const uint4*>(a6)[1];
+    s[0] = __builtin_bswap32(x.x); s[1] = __builtin_bswap32(x.y); s[2] = __builtin_bswap32(x.z); s[3] = __builtin_bswap32(x.w);
+    d[0] = __builtin_bswap32(y.x); d[1] = __builtin_bswap32(y.y); d[2] = __builtin_bswap32(y.z); d[3] = __builtin_bswap32(y.w);
   } else {
     s[0] = rec[0];
     d[0] = rec[1];
@@ -110,119 +113,276 @@ __device__ __forceinline__ void rtn_ct_make_key(const rtn_ct_args& a, rtn_u64 r,
   }
   k.w[8] = gt ? (sp << 16 | dp) : (dp << 16 | sp);
   k.w[9] = (k.tcp ? 6u : 17u) | (k.v6 ? 0x100u : 0u);
+  // two independent 32-bit chains; an IPv4 key's words 1-3 and 5-7 are zero and are skipped
   rtn_u32 f0 = 0x0C0FFEEu, f1 = 0x5EED5EEDu;
+  if (k.v6) {
 #pragma unroll
-  for (int j = 0; j < 10; ++j) {
-    f0 = rtn_ct_mix(f0, k.w[j]);
-    f1 = rtn_ct_mix(f1, k.w[j] ^ 0x9E3779B9u);
+    for (int j = 0; j < 10; ++j) {
+      f0 = rtn_ct_mix(f0, k.w[j]);
+      f1 = rtn_ct_mix(f1, k.w[j] ^ 0x9E3779B9u);
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 10; j += (j == 0 || j == 4) ? 4 : 1) {
+      f0 = rtn_ct_mix(f0, k.w[j]);
+      f1 = rtn_ct_mix(f1, k.w[j] ^ 0x9E3779B9u);
+    }
   }
   k.fp = ((rtn_u64)rtn_ct_fmix(f0 ^ 40u) << 32) | rtn_ct_fmix(f1 ^ 40u);
   if (k.fp < 2ull) k.fp += 2ull;
+}
+
+__device__ __forceinline__ bool rtn_ct_occupied(const rtn_u32* occ, rtn_u32 slot) {
+  return (occ[slot >> 5] >> (slot & 31u)) & 1u;
 }
 
 __device__ __forceinline__ rtn_u64* rtn_ct_tag(const rtn_ct_args& a, rtn_u32 slot) {
   return reinterpret_cast<rtn_u64*>(a.table + (rtn_u64)slot * 16u);
 }
 
-// Walk one chunk; fn(record index, ipv6 rank, frame index) for every forwarded frame.
-template <typename F>
-__device__ __forceinline__ void rtn_ct_walk(const rtn_ct_args& a, F&& fn) {
+#ifndef RTN_CT_GPW
+#define RTN_CT_GPW 4u  // 64-frame groups per wave: a chunk is one block of 8 / RTN_CT_GPW waves
+#endif
+#define RTN_CT_BLOCK (64u * (RTN_CT_CHUNK / 64u) / RTN_CT_GPW)
+
+// One block per 512-frame chunk; each wave takes RTN_CT_GPW groups and issues all of their loads
+// before using any (the walk is latency-bound: a wave per group left too few loads in flight).
+// The record rank comes from the chunk's 8 bitmap words; the IPv6 rank needs the IPv6 counts of
+// the earlier groups, exchanged through LDS. fn(lane has a record, record index, frame index,
+// record words, rtn_conn_t, IPv6 addresses or null) runs for every lane of every wave (lanes
+// without a record pass has == false) so that waves can cooperate inside it; it builds the key
+// only if it needs it.
+struct rtn_ct_frames {  // this lane's frame in each of the wave's RTN_CT_GPW groups
+  bool has[RTN_CT_GPW];
+  rtn_u64 r[RTN_CT_GPW], cv[RTN_CT_GPW];
+  rtn_u32 frame[RTN_CT_GPW];
+  rtn_u32 rec[RTN_CT_GPW][6];
+  const rtn_u32* a6[RTN_CT_GPW];
+};
+
+__device__ __forceinline__ void rtn_ct_load(const rtn_ct_args& a, rtn_ct_frames& f) {
+  constexpr rtn_u32 G = RTN_CT_GPW;
+  __shared__ rtn_u32 v6cnt[8];
   const rtn_u32 lane = threadIdx.x & 63u;
-  const rtn_u32 wave = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
-  const rtn_u32 nchunks = (a.n + RTN_CT_CHUNK - 1u) / RTN_CT_CHUNK;
-  if (wave >= nchunks) return;
+  const rtn_u32 w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const rtn_u32 c = blockIdx.x;
   const rtn_u64 lane_lt = lane ? (~0ull >> (64u - lane)) : 0ull;
-  const rtn_u32 gb = wave * (RTN_CT_CHUNK / 64u);
   const rtn_u32 nw = (a.n + 63u) / 64u;
-  const rtn_u32 ge = gb + RTN_CT_CHUNK / 64u < nw ? gb + RTN_CT_CHUNK / 64u : nw;
-  rtn_u32 nrec = 0, nv6 = 0;
-  for (rtn_u32 g = gb; g < ge; ++g) {
-    const rtn_u64 m = a.fwd_bm[g];
-    const bool mine = (m >> lane) & 1ull;
-    const rtn_u64 r = (rtn_u64)wave * RTN_CT_CHUNK + nrec + (rtn_u32)__popcll(m & lane_lt);
-    const bool v6 = mine && ((a.recs[r * 6u + 5u] >> 7) & 1u);
-    const rtn_u64 m6 = __ballot(v6);
-    const rtn_u64 v6r = (rtn_u64)wave * RTN_CT_CHUNK + nv6 + (rtn_u32)__popcll(m6 & lane_lt);
-    if (mine) fn(r, v6r, g * 64u + lane);
-    nrec += (rtn_u32)__popcll(m);
-    nv6 += (rtn_u32)__popcll(m6);
+  // the chunk's bitmap words: lane j < 8 holds word j; pre[j] = records before group j
+  const rtn_u32 gj = c * (RTN_CT_CHUNK / 64u) + (lane & 7u);
+  const rtn_u64 word = gj < nw ? a.fwd_bm[gj] : 0ull;
+  const rtn_u32 pop = (rtn_u32)__popcll(word);
+  rtn_u32 pre[8];
+  rtn_u32 acc = 0u;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    pre[j] = acc;
+    acc += __shfl(pop, j);
+  }
+  rtn_u64 m6[G];
+#pragma unroll
+  for (rtn_u32 u = 0; u < G; ++u) {
+    const rtn_u32 q = w * G + u;  // group within the chunk
+    const rtn_u64 m = __shfl(word, (int)q);
+    f.has[u] = c * (RTN_CT_CHUNK / 64u) + q < nw && ((m >> lane) & 1ull);
+    f.r[u] = (rtn_u64)c * RTN_CT_CHUNK + pre[q] + (rtn_u32)__popcll(m & lane_lt);
+    f.frame[u] = (c * (RTN_CT_CHUNK / 64u) + q) * 64u + lane;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) f.rec[u][j] = 0u;
+    f.cv[u] = 0ull;
+    if (f.has[u]) {
+      const uint2* rp = reinterpret_cast<const uint2*>(a.recs + f.r[u] * 6u);  // 8-byte aligned
+      const uint2 x0 = rp[0], x1 = rp[1], x2 = rp[2];
+      f.rec[u][0] = x0.x; f.rec[u][1] = x0.y; f.rec[u][2] = x1.x;
+      f.rec[u][3] = x1.y; f.rec[u][4] = x2.x; f.rec[u][5] = x2.y;
+      f.cv[u] = a.conn[f.r[u]];
+    }
+  }
+#pragma unroll
+  for (rtn_u32 u = 0; u < G; ++u) {
+    m6[u] = __ballot(f.has[u] && ((f.rec[u][5] >> 7) & 1u));
+    if (lane == 0u) v6cnt[w * G + u] = (rtn_u32)__popcll(m6[u]);
+  }
+  __syncthreads();
+#pragma unroll
+  for (rtn_u32 u = 0; u < G; ++u) {
+    const rtn_u32 q = w * G + u;
+    rtn_u32 v6base = 0u;
+    for (rtn_u32 j = 0; j < q; ++j) v6base += v6cnt[j];
+    const rtn_u64 v6r = (rtn_u64)c * RTN_CT_CHUNK + v6base + (rtn_u32)__popcll(m6[u] & lane_lt);
+    f.a6[u] = (m6[u] >> lane) & 1ull ? a.addr6 + v6r * 8u : nullptr;
   }
 }
 
-extern "C" __global__ void __launch_bounds__(256) rtn_ct_insert(rtn_ct_args a) {
-  rtn_ct_walk(a, [&](rtn_u64 r, rtn_u64 v6r, rtn_u32 frame) {
-    const rtn_u64 c = a.conn[r];
-    const rtn_u32 info = (rtn_u32)(c >> 32);
-    if (!((info >> 26) & 1u)) return;                 // cannot open a connection
-    const bool tcp = !((a.recs[r * 6u + 5u] >> 6) & 1u);
-    if (tcp && (info & 0x3ffffffu) == 0u) return;     // TCP opener dropped by filter_first_packet
-    rtn_ct_key k;
-    rtn_ct_make_key(a, r, v6r, k);
-    rtn_u32 slot = k.h & a.cap_mask;
-    for (rtn_u32 p = 0; p < RTN_CT_MAXPROBE; ++p, slot = (slot + 1u) & a.cap_mask) {
-      rtn_u64* tag = rtn_ct_tag(a, slot);
-      rtn_u64 t = __hip_atomic_load(tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (t == RTN_CT_EMPTY) {
-        if (atomicAdd(&a.live[0], 1u) >= a.max_live) {  // ConnTracker's max_connections
-          atomicSub(&a.live[0], 1u);
-          return;
-        }
-        const rtn_u64 old = atomicCAS(tag, RTN_CT_EMPTY, k.fp);
-        if (old == RTN_CT_EMPTY) {
-          rtn_u32* s = a.table + (rtn_u64)slot * 16u;
-          s[2] = a.epoch;
+extern "C" __global__ void __launch_bounds__(RTN_CT_BLOCK) rtn_ct_insert(rtn_ct_args a) {
+  constexpr rtn_u32 G = RTN_CT_GPW;
+  __shared__ rtn_u32 blk[3];  // openers needing a new slot (then tickets drawn), reservation base, granted
+  if (threadIdx.x == 0) blk[0] = 0u;
+  rtn_ct_frames f;
+  rtn_ct_load(a, f);
+  const rtn_u32 lane = threadIdx.x & 63u;
+  bool active[G];
+  rtn_u32 slot[G];
+  rtn_ct_key k[G];
 #pragma unroll
-          for (int j = 0; j < 10; ++j) s[4 + j] = k.w[j];
-          atomicMin(&s[3], frame);
-          return;
+  for (rtn_u32 u = 0; u < G; ++u) {
+    // openers: creates, and not a TCP opener dropped by filter_first_packet
+    const rtn_u32 info = (rtn_u32)(f.cv[u] >> 32);
+    const bool tcp = !((f.rec[u][5] >> 6) & 1u);
+    active[u] = f.has[u] && ((info >> 26) & 1u) && !(tcp && (info & 0x3ffffffu) == 0u);
+    if (active[u]) rtn_ct_make_key(a, f.rec[u], f.cv[u], f.a6[u], k[u]);
+    slot[u] = (rtn_u32)f.cv[u] & a.cap_mask;
+  }
+  // Phase A: find the key or the first empty slot of its probe chain (no writes).
+  bool at_empty[G];
+#pragma unroll
+  for (rtn_u32 u = 0; u < G; ++u) at_empty[u] = false;
+  for (rtn_u32 p = 0; p < RTN_CT_MAXPROBE; ++p) {
+    bool more = false;
+#pragma unroll
+    for (rtn_u32 u = 0; u < G; ++u) {
+      if (active[u] && !at_empty[u]) {
+        const rtn_u64 t = rtn_ct_occupied(a.occ, slot[u])
+                              ? __hip_atomic_load(rtn_ct_tag(a, slot[u]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                              : RTN_CT_EMPTY;
+        if (t == k[u].fp) {
+          atomicMin(&a.table[(rtn_u64)slot[u] * 16u + 3u], f.frame[u]);  // existing or claimed this batch
+          active[u] = false;
+        } else if (t == RTN_CT_EMPTY) {
+          at_empty[u] = true;
+        } else {
+          slot[u] = (slot[u] + 1u) & a.cap_mask;
+          more = true;
         }
-        atomicSub(&a.live[0], 1u);
-        t = old;
-      }
-      if (t == k.fp) {
-        atomicMin(&a.table[(rtn_u64)slot * 16u + 3u], frame);
-        return;
       }
     }
-  });
+    if (!__ballot(more)) break;
+  }
+  rtn_u32 want = 0u;
+#pragma unroll
+  for (rtn_u32 u = 0; u < G; ++u) {
+    active[u] = active[u] && at_empty[u];  // probe limit reached without an empty slot: full
+    want += (rtn_u32)__popcll(__ballot(active[u]));
+  }
+  // Admission (ConnTracker's size < max_connections): the block reserves one ticket per opener
+  // that still needs a slot with a single atomic (none once its connections exist) and returns
+  // the unused tickets at the end.
+  if (a.check) {
+    if (lane == 0u && want) atomicAdd(&blk[0], want);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const rtn_u32 all = blk[0];
+      const rtn_u32 b = all ? atomicAdd(&a.live[0], all) : 0u;
+      blk[1] = all;
+      blk[2] = b >= a.max_live ? 0u : (a.max_live - b < all ? a.max_live - b : all);
+      blk[0] = 0u;
+    }
+    __syncthreads();
+#pragma unroll
+    for (rtn_u32 u = 0; u < G; ++u) {
+      const rtn_u32 ticket = active[u] ? atomicAdd(&blk[0], 1u) : 0u;
+      if (active[u] && ticket >= blk[2]) active[u] = false;  // table full for this opener
+    }
+  }
+  // Phase B: claim from the empty slot on (another lane may take it first: keep probing).
+  rtn_u32 claims = 0u;
+  for (rtn_u32 p = 0; p < RTN_CT_MAXPROBE; ++p) {
+    bool more = false;
+#pragma unroll
+    for (rtn_u32 u = 0; u < G; ++u) {
+      if (active[u]) {
+        rtn_u64* tag = rtn_ct_tag(a, slot[u]);
+        rtn_u64 t = __hip_atomic_load(tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (t == RTN_CT_EMPTY) t = atomicCAS(tag, RTN_CT_EMPTY, k[u].fp);
+        if (t == RTN_CT_EMPTY) {
+          atomicOr(&a.occ[slot[u] >> 5], 1u << (slot[u] & 31u));
+          rtn_u32* s = a.table + (rtn_u64)slot[u] * 16u;
+          s[2] = a.epoch;
+#pragma unroll
+          for (int j = 0; j < 10; ++j) s[4 + j] = k[u].w[j];
+          atomicMin(&s[3], f.frame[u]);
+          active[u] = false;
+          ++claims;
+        } else if (t == k[u].fp) {
+          atomicMin(&a.table[(rtn_u64)slot[u] * 16u + 3u], f.frame[u]);
+          active[u] = false;
+        } else {
+          slot[u] = (slot[u] + 1u) & a.cap_mask;
+          more = true;
+        }
+      }
+    }
+    if (!__ballot(more)) break;
+  }
+  rtn_u32 n = claims;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) n += __shfl_xor(n, d);
+  if (a.check) {
+    // return the reserved tickets that did not become a connection
+    __syncthreads();
+    if (threadIdx.x == 0) blk[0] = 0u;
+    __syncthreads();
+    if (lane == 0u && n) atomicAdd(&blk[0], n);
+    __syncthreads();
+    if (threadIdx.x == 0 && blk[1] > blk[0]) atomicSub(&a.live[0], blk[1] - blk[0]);
+  } else if (lane == 0u && n) {
+    // one atomic per wave, spread over 64 counters (live = their sum)
+    atomicAdd(&a.live[(blockIdx.x * 8u + (threadIdx.x >> 6)) & 63u], n);
+  }
 }
 
-extern "C" __global__ void __launch_bounds__(256) rtn_ct_lookup(rtn_ct_args a) {
-  rtn_ct_walk(a, [&](rtn_u64 r, rtn_u64 v6r, rtn_u32 frame) {
-    rtn_ct_key k;
-    rtn_ct_make_key(a, r, v6r, k);
-    const bool opens = (k.info >> 26) & 1u;
-    const bool dropped = k.tcp && (k.info & 0x3ffffffu) == 0u;
-    rtn_u32 slot = k.h & a.cap_mask, status = 0u, found = 0xffffffffu;
-    for (rtn_u32 p = 0; p < RTN_CT_MAXPROBE; ++p, slot = (slot + 1u) & a.cap_mask) {
-      const rtn_u32* s = a.table + (rtn_u64)slot * 16u;
-      const rtn_u64 t = *reinterpret_cast<const rtn_u64*>(s);
-      if (t == RTN_CT_EMPTY) break;
-      if (t != k.fp) continue;
-      bool same = true;
+extern "C" __global__ void __launch_bounds__(RTN_CT_BLOCK) rtn_ct_lookup(rtn_ct_args a) {
+  rtn_ct_frames f;
+  rtn_ct_load(a, f);
+  // the start slots' occupancy bits first, for every group (most misses end here, in L2)
+  bool occ0[RTN_CT_GPW];
 #pragma unroll
-      for (int j = 0; j < 10; ++j) same = same && s[4 + j] == k.w[j];
-      if (!same) {
-        status = RTN_CT_COLLISION;
+  for (rtn_u32 u = 0; u < RTN_CT_GPW; ++u)
+#ifdef RTN_CT_EXP_NO_PROBE
+    occ0[u] = false;  // experiment: loads, status and store only
+#else
+    occ0[u] = f.has[u] && rtn_ct_occupied(a.occ, (rtn_u32)f.cv[u] & a.cap_mask);
+#endif
+#pragma unroll
+  for (rtn_u32 u = 0; u < RTN_CT_GPW; ++u) {
+    if (!f.has[u]) continue;
+    const rtn_u64 cv = f.cv[u];
+    const rtn_u32 info = (rtn_u32)(cv >> 32), frame = f.frame[u];
+    const bool opens = (info >> 26) & 1u;
+    const bool dropped = !((f.rec[u][5] >> 6) & 1u) && (info & 0x3ffffffu) == 0u;
+    rtn_u32 slot = (rtn_u32)cv & a.cap_mask, status = 0u, found = 0xffffffffu;
+    if (occ0[u]) {
+      rtn_ct_key k;
+      rtn_ct_make_key(a, f.rec[u], cv, f.a6[u], k);
+      for (rtn_u32 p = 0; p < RTN_CT_MAXPROBE; ++p, slot = (slot + 1u) & a.cap_mask) {
+        if (p > 0u && !rtn_ct_occupied(a.occ, slot)) break;
+        const rtn_u32* s = a.table + (rtn_u64)slot * 16u;
+        const rtn_u64 t = *reinterpret_cast<const rtn_u64*>(s);
+        if (t == RTN_CT_EMPTY) break;
+        if (t != k.fp) continue;
+        bool same = true;
+#pragma unroll
+        for (int j = 0; j < 10; ++j) same = same && s[4 + j] == k.w[j];
+        if (!same) {
+          status = RTN_CT_COLLISION;
+          break;
+        }
+        found = slot;
+        if (s[2] != a.epoch) {
+          status = RTN_CT_HIT | RTN_CT_PRIOR;
+        } else {
+          const rtn_u32 first = s[3];
+          status = frame > first ? RTN_CT_HIT : frame == first ? RTN_CT_NEW : (opens ? RTN_CT_NEW_DROPPED : RTN_CT_MISS);
+        }
         break;
       }
-      found = slot;
-      if (s[2] != a.epoch) {
-        status = RTN_CT_HIT | RTN_CT_PRIOR;
-      } else {
-        const rtn_u32 first = s[3];
-        status = frame > first ? RTN_CT_HIT : frame == first ? RTN_CT_NEW : (opens ? RTN_CT_NEW_DROPPED : RTN_CT_MISS);
-      }
-      break;
     }
     if (status == 0u) status = !opens ? RTN_CT_MISS : dropped ? RTN_CT_NEW_DROPPED : RTN_CT_FULL;
     if (status == RTN_CT_COLLISION) found = 0xffffffffu;
-    a.out[r] = (rtn_u64)found | ((rtn_u64)status << 32);
-  });
+    a.out[f.r[u]] = (rtn_u64)found | ((rtn_u64)status << 32);
+  }
 }
 
-// Host-requested removals (terminated / expired / dropped connections): the slots become
-// tombstones (probe chains stay intact); rtn_ct_rebuild compacts them away.
 extern "C" __global__ void __launch_bounds__(256) rtn_ct_remove_k(rtn_u32* table, rtn_u32* live, const rtn_u32* slots,
                                                                  rtn_u32 n, rtn_u32 cap_mask) {
   const rtn_u32 i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -250,7 +410,8 @@ extern "C" __global__ void __launch_bounds__(256) rtn_ct_clear(rtn_u32* table, r
 // Rebuild: move the live slots of `src` into the cleared table `dst` (same capacity), dropping
 // tombstones. Keys and epochs move; `first` restarts at 0xffffffff. new_slot[i] = where slot i
 // went (0xffffffff if it was not live) so the host can re-index its per-connection state.
-extern "C" __global__ void __launch_bounds__(256) rtn_ct_rehash(const rtn_u32* src, rtn_u32* dst, rtn_u32* new_slot,
+extern "C" __global__ void __launch_bounds__(256) rtn_ct_rehash(const rtn_u32* src, rtn_u32* dst, rtn_u32* dst_occ,
+                                                               rtn_u32* new_slot,
                                                                rtn_u32 cap_mask) {
   const rtn_u64 i = (rtn_u64)blockIdx.x * blockDim.x + threadIdx.x;
   if (i > cap_mask) return;
@@ -277,6 +438,7 @@ extern "C" __global__ void __launch_bounds__(256) rtn_ct_rehash(const rtn_u32* s
   for (rtn_u32 p = 0; p <= cap_mask; ++p, slot = (slot + 1u) & cap_mask) {
     rtn_u64* tag = reinterpret_cast<rtn_u64*>(dst + (rtn_u64)slot * 16u);
     if (atomicCAS(tag, RTN_CT_EMPTY, t) == RTN_CT_EMPTY) {
+      atomicOr(&dst_occ[slot >> 5], 1u << (slot & 31u));
       rtn_u32* d = dst + (rtn_u64)slot * 16u;
       d[2] = s[2];
 #pragma unroll

@@ -42,13 +42,23 @@ size_t copy_text(const std::string& s, char* buf, size_t cap) {
   return s.size();
 }
 
+std::string env_defines();
+
 std::string build_source(const rtn::PacketProgram& prog) {
   const std::string tpl = kPcKernelSrc;
   const std::string marker = "//@@RTN_FILTER@@";
   size_t at = tpl.find(marker);
   std::string head = "#define RTN_DELIVER_WORDS " + std::to_string(prog.deliver_words()) + "\n" +
-                     "#define RTN_CONN_WORDS " + std::to_string(prog.conn_deliver_words()) + "\n";
-  // Kernel variants for experiments (e.g. "RTN_NO_PREFETCH"); never set in production runs.
+                     "#define RTN_CONN_WORDS " + std::to_string(prog.conn_deliver_words()) + "\n" + env_defines();
+  std::string src = head + tpl.substr(0, at) + prog.hip_body + tpl.substr(at + marker.size());
+  const std::string cmarker = "//@@RTN_CONN_FILTER@@";
+  size_t cat = src.find(cmarker);
+  return src.substr(0, cat) + prog.hip_conn_body + src.substr(cat + cmarker.size());
+}
+
+// Kernel variants for experiments (RTN_KERNEL_DEFINES="A,B=1"); never set in production runs.
+std::string env_defines() {
+  std::string head;
   if (const char* d = getenv("RTN_KERNEL_DEFINES")) {
     std::string all = d, tok;
     for (size_t k = 0; k <= all.size(); ++k) {
@@ -60,10 +70,7 @@ std::string build_source(const rtn::PacketProgram& prog) {
       }
     }
   }
-  std::string src = head + tpl.substr(0, at) + prog.hip_body + tpl.substr(at + marker.size());
-  const std::string cmarker = "//@@RTN_CONN_FILTER@@";
-  size_t cat = src.find(cmarker);
-  return src.substr(0, cat) + prog.hip_conn_body + src.substr(cat + cmarker.size());
+  return head;
 }
 
 std::string json_str(const std::string& s) {
@@ -429,13 +436,17 @@ size_t rtn_out_conn_dlv_bytes(uint32_t n, uint32_t conn_words) { return chunked(
 struct rtn_ct {
   int device = 0;
   uint32_t cap = 0, max_live = 0, epoch = 0;
+  uint64_t live_bound = 0;   // upper bound of the live connections (exact after a fold)
   uint32_t* table = nullptr;
-  uint32_t* live = nullptr;  // [0] live slots
+  uint32_t* occ = nullptr;   // cap bits
+  uint32_t* live = nullptr;  // [64] counters, live = their sum (mod 2^32)
   hipModule_t module = nullptr;
   hipFunction_t insert = nullptr, lookup = nullptr, remove = nullptr, clear = nullptr, rehash = nullptr;
 };
 
 namespace {
+constexpr uint32_t RTN_CT_GPW = 4;  // must match ct_kernel.hip
+
 struct CtArgs {  // must match struct rtn_ct_args in ct_kernel.hip
   const uint64_t* fwd_bm;
   const uint32_t* recs;
@@ -443,14 +454,33 @@ struct CtArgs {  // must match struct rtn_ct_args in ct_kernel.hip
   const uint64_t* conn;
   uint64_t* out;
   uint32_t* table;
+  uint32_t* occ;
   uint32_t* live;
   uint32_t n;
   uint32_t cap_mask;
   uint32_t max_live;
   uint32_t epoch;
+  uint32_t check;
 };
 
 int32_t hip_fail(const char* what, hipError_t e) { return fail(RTN_EDEVICE, std::string(what) + ": " + hipGetErrorString(e)); }
+
+// Exact live count: wait for the stream, sum the 64 counters and fold them into counter 0.
+int32_t ct_fold(rtn_ct* ct, hipStream_t s, uint32_t* live_out) {
+  uint32_t c[64];
+  hipError_t e = s ? hipStreamSynchronize(s) : hipDeviceSynchronize();
+  if (e == hipSuccess) e = hipMemcpy(c, ct->live, sizeof(c), hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return hip_fail("ct_fold", e);
+  uint32_t sum = 0;
+  for (uint32_t v : c) sum += v;
+  uint32_t z[64] = {};
+  z[0] = sum;
+  e = hipMemcpy(ct->live, z, sizeof(z), hipMemcpyHostToDevice);
+  if (e != hipSuccess) return hip_fail("ct_fold", e);
+  ct->live_bound = sum;
+  *live_out = sum;
+  return RTN_OK;
+}
 
 int32_t ct_clear(rtn_ct* ct, uint32_t* table, hipStream_t s) {
   uint32_t cap = ct->cap;
@@ -466,7 +496,7 @@ int32_t rtn_ct_create(int device, uint32_t capacity_log2, uint32_t max_connectio
   if (!out) return fail(RTN_EINVAL, "null argument");
   if (capacity_log2 < 6 || capacity_log2 > 30) return fail(RTN_EINVAL, "capacity_log2 must be in [6, 30]");
   std::shared_ptr<std::vector<uint8_t>> code;
-  int32_t rc = compile_code_object(kCtKernelSrc, code);
+  int32_t rc = compile_code_object(env_defines() + kCtKernelSrc, code);
   if (rc) return rc;
   auto ct = std::make_unique<rtn_ct>();
   ct->device = device;
@@ -483,9 +513,13 @@ int32_t rtn_ct_create(int device, uint32_t capacity_log2, uint32_t max_connectio
   }
   e = hipMalloc(reinterpret_cast<void**>(&ct->table), (size_t)ct->cap * 64u);
   if (e != hipSuccess) return hip_fail("hipMalloc(table)", e);
-  e = hipMalloc(reinterpret_cast<void**>(&ct->live), 16);
+  e = hipMalloc(reinterpret_cast<void**>(&ct->occ), ct->cap / 8u);
+  if (e != hipSuccess) return hip_fail("hipMalloc(occ)", e);
+  e = hipMemset(ct->occ, 0, ct->cap / 8u);
+  if (e != hipSuccess) return hip_fail("hipMemset(occ)", e);
+  e = hipMalloc(reinterpret_cast<void**>(&ct->live), 64 * 4);
   if (e != hipSuccess) return hip_fail("hipMalloc", e);
-  e = hipMemset(ct->live, 0, 16);
+  e = hipMemset(ct->live, 0, 64 * 4);
   if (e != hipSuccess) return hip_fail("hipMemset", e);
   rc = ct_clear(ct.get(), ct->table, nullptr);
   if (rc) return rc;
@@ -498,6 +532,7 @@ int32_t rtn_ct_create(int device, uint32_t capacity_log2, uint32_t max_connectio
 int32_t rtn_ct_destroy(rtn_ct_t* ct) {
   if (!ct) return RTN_OK;
   if (ct->table) (void)hipFree(ct->table);
+  if (ct->occ) (void)hipFree(ct->occ);
   if (ct->live) (void)hipFree(ct->live);
   if (ct->module) (void)hipModuleUnload(ct->module);
   delete ct;
@@ -516,18 +551,24 @@ int32_t rtn_ct_process(rtn_ct_t* ct, const rtn_pc_out_t* pc, uint32_t n, rtn_ct_
   a.conn = reinterpret_cast<const uint64_t*>(pc->conn);
   a.out = reinterpret_cast<uint64_t*>(out);
   a.table = ct->table;
+  a.occ = ct->occ;
   a.live = ct->live;
   a.n = n;
   a.cap_mask = ct->cap - 1u;
   a.max_live = ct->max_live;
   a.epoch = ++ct->epoch;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const uint32_t chunks = (n + RTN_CHUNK_FRAMES - 1u) / RTN_CHUNK_FRAMES;
-  const uint32_t blocks = (chunks + 3u) / 4u;  // one wave per chunk
+  // Admission against max_connections on the device: one reservation atomic per block that
+  // opens connections (RTN_CT_SPREAD_COUNTERS=1 in the environment selects the unchecked variant
+  // with spread counters, for experiments).
+  static const bool spread = getenv("RTN_CT_SPREAD_COUNTERS") != nullptr;
+  a.check = spread ? 0u : 1u;
+  const uint32_t chunks = (n + RTN_CHUNK_FRAMES - 1u) / RTN_CHUNK_FRAMES;  // one 512-thread block each
   void* p[] = {&a};
-  hipError_t e = hipModuleLaunchKernel(ct->insert, blocks, 1, 1, 256, 1, 1, 0, s, p, nullptr);
+  const uint32_t threads = 512u / RTN_CT_GPW;  // ct_kernel.hip: a chunk per block, RTN_CT_GPW groups per wave
+  hipError_t e = hipModuleLaunchKernel(ct->insert, chunks, 1, 1, threads, 1, 1, 0, s, p, nullptr);
   if (e != hipSuccess) return hip_fail("rtn_ct_insert", e);
-  e = hipModuleLaunchKernel(ct->lookup, blocks, 1, 1, 256, 1, 1, 0, s, p, nullptr);
+  e = hipModuleLaunchKernel(ct->lookup, chunks, 1, 1, threads, 1, 1, 0, s, p, nullptr);
   if (e != hipSuccess) return hip_fail("rtn_ct_lookup", e);
   return RTN_OK;
 }
@@ -547,33 +588,43 @@ int32_t rtn_ct_remove(rtn_ct_t* ct, const uint32_t* slots, uint32_t n, void* str
 int32_t rtn_ct_rebuild(rtn_ct_t* ct, uint32_t* new_slot, void* stream) {
   if (!ct || !new_slot) return fail(RTN_EINVAL, "null argument");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  uint32_t* dst = nullptr;
+  uint32_t *dst = nullptr, *docc = nullptr;
   hipError_t e = hipMalloc(reinterpret_cast<void**>(&dst), (size_t)ct->cap * 64u);
-  if (e != hipSuccess) return hip_fail("hipMalloc(rebuild)", e);
+  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&docc), ct->cap / 8u);
+  if (e == hipSuccess) e = hipMemsetAsync(docc, 0, ct->cap / 8u, s);
+  if (e != hipSuccess) {
+    if (dst) (void)hipFree(dst);
+    if (docc) (void)hipFree(docc);
+    return hip_fail("rtn_ct_rebuild alloc", e);
+  }
   int32_t rc = ct_clear(ct, dst, s);
   if (rc) {
     (void)hipFree(dst);
+    (void)hipFree(docc);
     return rc;
   }
   const uint32_t* src = ct->table;
   uint32_t mask = ct->cap - 1u;
-  void* p[] = {&src, &dst, &new_slot, &mask};
+  void* p[] = {&src, &dst, &docc, &new_slot, &mask};
   e = hipModuleLaunchKernel(ct->rehash, (ct->cap + 255u) / 256u, 1, 1, 256, 1, 1, 0, s, p, nullptr);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (e != hipSuccess) {
     (void)hipFree(dst);
+    (void)hipFree(docc);
     return hip_fail("rtn_ct_rehash", e);
   }
   (void)hipFree(ct->table);
+  (void)hipFree(ct->occ);
   ct->table = dst;
+  ct->occ = docc;
   return RTN_OK;
 }
 
 int32_t rtn_ct_stats(rtn_ct_t* ct, rtn_ct_stats_t* st) {
   if (!ct || !st) return fail(RTN_EINVAL, "null argument");
   uint32_t live = 0;
-  hipError_t e = hipMemcpy(&live, ct->live, 4, hipMemcpyDeviceToHost);
-  if (e != hipSuccess) return hip_fail("hipMemcpy", e);
+  int32_t rc = ct_fold(ct, nullptr, &live);
+  if (rc) return rc;
   st->capacity = ct->cap;
   st->live = live;
   st->epoch = ct->epoch;
