@@ -273,13 +273,18 @@ def main() -> None:
         c1.record(stream)
         torch.cuda.synchronize(dev)
         cms = c0.elapsed_time(c1) / args.steps
-        # connection lookup (include/retina_ct.h) over the same batch: insert + lookup launches on a
-        # 2^24-slot (1 GiB) table; the first pass opens every SYN-only/UDP flow, the timed passes
-        # then find them (Occupied) and drop the rest (Vacant, not an opener)
-        ct = pc.ConnTable(local, 24)
-        ct_out = ct.process(cout, stream=stream)
+        # connection lookup (include/retina_ct.h) over the same batch, on a 2^25-slot (2 GiB)
+        # table admitting 10 M connections (configs/online.toml max_connections): the first pass
+        # opens every SYN-only/UDP flow of the batch, the timed passes find them (Occupied) and
+        # drop the rest (Vacant, not an opener)
+        ct = pc.ConnTable(local, 25, 10_000_000)
         k0 = torch.cuda.Event(enable_timing=True)
         k1 = torch.cuda.Event(enable_timing=True)
+        k0.record(stream)
+        ct_out = ct.process(cout, stream=stream)
+        k1.record(stream)
+        torch.cuda.synchronize(dev)
+        ct_first = k0.elapsed_time(k1)
         k0.record(stream)
         for _ in range(args.steps):
             ct.process(cout, out=ct_out, stream=stream)
@@ -292,6 +297,7 @@ def main() -> None:
                       "vs_filter_only": round(kern_ms / cms, 3),
                       "first_packet_tree_size": prog.info["conn_tree_size"],
                       "ct_lookup": {"ms": round(ctms, 4), "mpps": round(n / ctms / 1e3, 1),
+                                    "first_pass_ms": round(ct_first, 4), "opened_first_pass": ct_stats["live"],
                                     "forwarded_per_s_M": round(counters_fwd_hint(cout) / ctms / 1e3, 1),
                                     "table_slots": ct_stats["capacity"], "live": ct_stats["live"]},
                       "note": "same step + rtn_conn_t (8 B) per forwarded frame: ConnId hash/orientation, "

@@ -191,11 +191,15 @@ __device__ __forceinline__ void rtn_ct_load(const rtn_ct_args& a, rtn_ct_frames&
     for (int j = 0; j < 6; ++j) f.rec[u][j] = 0u;
     f.cv[u] = 0ull;
     if (f.has[u]) {
-      const uint2* rp = reinterpret_cast<const uint2*>(a.recs + f.r[u] * 6u);  // 8-byte aligned
-      const uint2 x0 = rp[0], x1 = rp[1], x2 = rp[2];
-      f.rec[u][0] = x0.x; f.rec[u][1] = x0.y; f.rec[u][2] = x1.x;
-      f.rec[u][3] = x1.y; f.rec[u][4] = x2.x; f.rec[u][5] = x2.y;
-      f.cv[u] = a.conn[f.r[u]];
+      // streamed once: non-temporal, so the occupancy bitmap keeps its place in L2
+      const rtn_u64* rp = reinterpret_cast<const rtn_u64*>(a.recs + f.r[u] * 6u);  // 8-byte aligned
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const rtn_u64 x = __builtin_nontemporal_load(rp + j);
+        f.rec[u][2 * j] = (rtn_u32)x;
+        f.rec[u][2 * j + 1] = (rtn_u32)(x >> 32);
+      }
+      f.cv[u] = __builtin_nontemporal_load(a.conn + f.r[u]);
     }
   }
 #pragma unroll
@@ -246,7 +250,10 @@ extern "C" __global__ void __launch_bounds__(RTN_CT_BLOCK) rtn_ct_insert(rtn_ct_
                               ? __hip_atomic_load(rtn_ct_tag(a, slot[u]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                               : RTN_CT_EMPTY;
         if (t == k[u].fp) {
-          atomicMin(&a.table[(rtn_u64)slot[u] * 16u + 3u], f.frame[u]);  // existing or claimed this batch
+          // `first` only matters for a slot opened in this batch (epoch == this batch, or 0 while
+          // its claimer is still writing it); an older connection's frames are plain hits
+          const rtn_u32 ep = a.table[(rtn_u64)slot[u] * 16u + 2u];
+          if (ep == 0u || ep == a.epoch) atomicMin(&a.table[(rtn_u64)slot[u] * 16u + 3u], f.frame[u]);
           active[u] = false;
         } else if (t == RTN_CT_EMPTY) {
           at_empty[u] = true;
@@ -331,55 +338,94 @@ extern "C" __global__ void __launch_bounds__(RTN_CT_BLOCK) rtn_ct_insert(rtn_ct_
   }
 }
 
+// status of a frame whose key sits at slot s (epoch / first decide the branch)
+__device__ __forceinline__ rtn_u32 rtn_ct_status(const rtn_ct_args& a, rtn_u32 epoch, rtn_u32 first, rtn_u32 frame,
+                                                 bool opens) {
+  if (epoch != a.epoch) return RTN_CT_HIT | RTN_CT_PRIOR;
+  return frame > first ? RTN_CT_HIT : frame == first ? RTN_CT_NEW : (opens ? RTN_CT_NEW_DROPPED : RTN_CT_MISS);
+}
+
 extern "C" __global__ void __launch_bounds__(RTN_CT_BLOCK) rtn_ct_lookup(rtn_ct_args a) {
+  constexpr rtn_u32 G = RTN_CT_GPW;
   rtn_ct_frames f;
   rtn_ct_load(a, f);
-  // the start slots' occupancy bits first, for every group (most misses end here, in L2)
-  bool occ0[RTN_CT_GPW];
+  // Every group's first probe is issued before any is used: the start slot's occupancy bit (in
+  // L2; most misses end here), then the tags of occupied start slots, then the slots whose tag
+  // matches. Only chains (start slot held by another key or removed) probe further, one by one.
+  bool occ0[G], occx[G] = {};
 #pragma unroll
-  for (rtn_u32 u = 0; u < RTN_CT_GPW; ++u)
-#ifdef RTN_CT_EXP_NO_PROBE
+  for (rtn_u32 u = 0; u < G; ++u) {
+#if defined(RTN_CT_EXP_NO_PROBE)
     occ0[u] = false;  // experiment: loads, status and store only
+#elif defined(RTN_CT_EXP_OCC_ONLY)
+    occ0[u] = false;  // experiment: the occupancy reads only (kept alive in the store)
+    occx[u] = f.has[u] && rtn_ct_occupied(a.occ, (rtn_u32)f.cv[u] & a.cap_mask);
 #else
     occ0[u] = f.has[u] && rtn_ct_occupied(a.occ, (rtn_u32)f.cv[u] & a.cap_mask);
 #endif
+  }
+  // an occupied start slot is read whole (tag, epoch, first, key: one 64-B line) in one go
+  rtn_ct_key k[G];
+  rtn_u64 t[G];
+  uint4 s0[G], s1[G], s2[G];  // words 0-11 (tag, epoch, first, key 0-7); key 8-9 in s3
+  uint2 s3[G];
 #pragma unroll
-  for (rtn_u32 u = 0; u < RTN_CT_GPW; ++u) {
+  for (rtn_u32 u = 0; u < G; ++u) {
+    t[u] = RTN_CT_EMPTY;
+    if (occ0[u]) {
+      const uint4* sp = reinterpret_cast<const uint4*>(a.table + (rtn_u64)((rtn_u32)f.cv[u] & a.cap_mask) * 16u);
+      s0[u] = sp[0];
+      s1[u] = sp[1];
+      s2[u] = sp[2];
+      s3[u] = reinterpret_cast<const uint2*>(sp + 3)[0];
+      rtn_ct_make_key(a, f.rec[u], f.cv[u], f.a6[u], k[u]);
+      t[u] = (rtn_u64)s0[u].x | ((rtn_u64)s0[u].y << 32);
+    }
+  }
+#pragma unroll
+  for (rtn_u32 u = 0; u < G; ++u) {
     if (!f.has[u]) continue;
     const rtn_u64 cv = f.cv[u];
     const rtn_u32 info = (rtn_u32)(cv >> 32), frame = f.frame[u];
     const bool opens = (info >> 26) & 1u;
     const bool dropped = !((f.rec[u][5] >> 6) & 1u) && (info & 0x3ffffffu) == 0u;
     rtn_u32 slot = (rtn_u32)cv & a.cap_mask, status = 0u, found = 0xffffffffu;
-    if (occ0[u]) {
-      rtn_ct_key k;
-      rtn_ct_make_key(a, f.rec[u], cv, f.a6[u], k);
-      for (rtn_u32 p = 0; p < RTN_CT_MAXPROBE; ++p, slot = (slot + 1u) & a.cap_mask) {
-        if (p > 0u && !rtn_ct_occupied(a.occ, slot)) break;
-        const rtn_u32* s = a.table + (rtn_u64)slot * 16u;
-        const rtn_u64 t = *reinterpret_cast<const rtn_u64*>(s);
-        if (t == RTN_CT_EMPTY) break;
-        if (t != k.fp) continue;
+    if (occ0[u] && t[u] == k[u].fp) {
+      const rtn_u32 w[10] = {s1[u].x, s1[u].y, s1[u].z, s1[u].w, s2[u].x, s2[u].y, s2[u].z, s2[u].w, s3[u].x, s3[u].y};
+      bool same = true;
+#pragma unroll
+      for (int j = 0; j < 10; ++j) same = same && w[j] == k[u].w[j];
+      if (same) {
+        found = slot;
+        status = rtn_ct_status(a, s0[u].z, s0[u].w, frame, opens);
+      } else {
+        status = RTN_CT_COLLISION;
+      }
+    } else if (occ0[u] && t[u] != RTN_CT_EMPTY) {
+      // the start slot holds another key (or was removed): walk the chain
+      for (rtn_u32 p = 1; p < RTN_CT_MAXPROBE; ++p) {
+        slot = (slot + 1u) & a.cap_mask;
+        if (!rtn_ct_occupied(a.occ, slot)) break;
+        const rtn_u32* sp = a.table + (rtn_u64)slot * 16u;
+        const rtn_u64 tt = *reinterpret_cast<const rtn_u64*>(sp);
+        if (tt == RTN_CT_EMPTY) break;
+        if (tt != k[u].fp) continue;
         bool same = true;
 #pragma unroll
-        for (int j = 0; j < 10; ++j) same = same && s[4 + j] == k.w[j];
+        for (int j = 0; j < 10; ++j) same = same && sp[4 + j] == k[u].w[j];
         if (!same) {
           status = RTN_CT_COLLISION;
           break;
         }
         found = slot;
-        if (s[2] != a.epoch) {
-          status = RTN_CT_HIT | RTN_CT_PRIOR;
-        } else {
-          const rtn_u32 first = s[3];
-          status = frame > first ? RTN_CT_HIT : frame == first ? RTN_CT_NEW : (opens ? RTN_CT_NEW_DROPPED : RTN_CT_MISS);
-        }
+        status = rtn_ct_status(a, sp[2], sp[3], frame, opens);
         break;
       }
     }
     if (status == 0u) status = !opens ? RTN_CT_MISS : dropped ? RTN_CT_NEW_DROPPED : RTN_CT_FULL;
     if (status == RTN_CT_COLLISION) found = 0xffffffffu;
-    a.out[f.r[u]] = (rtn_u64)found | ((rtn_u64)status << 32);
+    if (occx[u]) status |= 0x80000000u;
+    __builtin_nontemporal_store((rtn_u64)found | ((rtn_u64)status << 32), a.out + f.r[u]);
   }
 }
 
