@@ -37,12 +37,21 @@ def main(tag: str, cfg: str, frames: int) -> None:
     # the dominant packet-stage kernel (rtn_pc_kernel_s64 for 64-byte slots, rtn_pc_kernel otherwise)
     name = max((n for n in stats if n.startswith(KERNEL)), key=lambda n: float(stats[n]["TotalDurationNs"]))
     k = stats[name]
+    # per-launch durations: bench.py runs warm-up + timed launches on preallocated outputs, then
+    # one launch on freshly allocated outputs for the totals (first-touch of new buffers makes that
+    # one slow); the bench's HIP-event figure corresponds to the launches before it
+    trace = [r for r in csv.DictReader(open(out / f"prof_{tag}_{cfg}" / "run_kernel_trace.csv"))
+             if r["Kernel_Name"] == name]
+    durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in trace]
+    steady = durs[:-1] if len(durs) > 1 else durs
     fetch = counter(out / f"pmc_{tag}_{cfg}_FETCH_SIZE" / "run_counter_collection.csv")
     write = counter(out / f"pmc_{tag}_{cfg}_WRITE_SIZE" / "run_counter_collection.csv")
     f_kb, w_kb = statistics.median(fetch), statistics.median(write)
     d = {
         "tag": tag, "config": cfg, "frames": frames, "kernel": name,
         "kernel_avg_ns": float(k["AverageNs"]), "kernel_calls": int(k["Calls"]),
+        "kernel_avg_ns_preallocated_outputs": statistics.mean(steady),
+        "kernel_median_ns": statistics.median(durs), "kernel_durations_ns": durs,
         "fetch_size_kib_median": f_kb, "write_size_kib_median": w_kb, "pmc_dispatches": [len(fetch), len(write)],
         "read_bytes_per_launch": int(2 * f_kb * 1024), "write_bytes_per_launch": int(w_kb * 1024),
         "hbm_bytes_per_launch": int(2 * f_kb * 1024 + w_kb * 1024),
