@@ -156,6 +156,10 @@ size_t rtn_program_source(const rtn_program_t* p, char* buf, size_t cap); /* ful
 /* Statement k of a deliver mask -> subscription index / Payload flag. */
 int32_t rtn_program_deliver_table(const rtn_program_t* p, uint32_t* sub_ids, uint8_t* is_payload,
                                   uint32_t cap);
+/* The packet-level keep/drop filter for the NIC (FilterFactory.filter_str, get_hw_filter in
+ * filtergen/src/lib.rs:233-238): the PacketContinue tree's paths joined with "or" ("" = keep all).
+ * Installing it as rte_flow rules (core/src/filter/hardware) is the caller's business. */
+size_t rtn_program_hw_filter(const rtn_program_t* p, char* buf, size_t cap);
 /* The first-packet filter (FilterLayer::Packet): its tree, its filtergen view, and statement
  * k of a conn_dlv mask -> subscription index / RTN_STMT_* kind. */
 size_t rtn_program_conn_tree(const rtn_program_t* p, char* buf, size_t cap);

@@ -1112,6 +1112,26 @@ class PacketTree:
         number(self.root)
         self.size = counter[0]
 
+    def to_filter_string(self) -> str:
+        """PTree::to_filter_string (ptree.rs:841-870): root-to-leaf paths, "and"-joined
+        predicates in parentheses, paths "or"-joined; "" for a childless root."""
+        if not self.root.kids:
+            return ""
+        out = []
+
+        def rec(n, curr):
+            curr = "(" if not curr else curr + f"({n.pred})"
+            if not n.kids:
+                out.append(curr + ")")
+                return
+            if curr != "(":
+                curr += " and "
+            for k in n.kids:
+                rec(k, curr)
+
+        rec(self.root, "")
+        return " or ".join(out)
+
     def pprint(self) -> str:
         lines = []
 

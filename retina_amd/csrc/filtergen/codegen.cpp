@@ -330,6 +330,14 @@ PacketProgram compile_packet_program(const std::vector<SubscriptionSpec>& subs) 
     (void)filter_subtree(l, prog.subs);
   prog.tree = filter_subtree(FilterLayer::PacketContinue, prog.subs);
   prog.conn_tree = filter_subtree(FilterLayer::Packet, prog.subs);
+  // get_hw_filter (filtergen/src/lib.rs:233-238): the PacketContinue tree's paths as one filter
+  // string, which filtergen re-parses and panics on if invalid ("Invalid HW filter")
+  prog.hw_filter = prog.tree.to_filter_string();
+  try {
+    (void)Filter::make(prog.hw_filter);
+  } catch (const FilterError& e) {
+    throw FilterError("Invalid HW filter " + prog.hw_filter + ": " + e.what());
+  }
   const PNode& root = prog.tree.root;
   if (root.actions.terminal != 0) throw FilterError("internal: terminal actions at PacketContinue");
 

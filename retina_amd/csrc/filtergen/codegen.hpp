@@ -37,6 +37,7 @@ struct PacketProgram {
   std::string hip_body;     // __device__ function rtn_filter(...) specialised to this tree
   std::string rust_listing; // the Rust the reference filtergen would emit (normalised), for review
   bool wraps_ethernet = false;
+  std::string hw_filter;    // get_hw_filter (filtergen/src/lib.rs:233-238): the NIC keep/drop filter
   uint32_t deliver_words() const { return (uint32_t)((delivers.size() + 63) / 64); }
 
   // first-packet filter (FilterLayer::Packet, the generated `packet_filter`, filtergen/src/lib.rs:284-285)

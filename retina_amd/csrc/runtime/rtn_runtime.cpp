@@ -255,6 +255,9 @@ int32_t rtn_program_info(const rtn_program_t* p, rtn_program_info_t* info) {
   return RTN_OK;
 }
 
+size_t rtn_program_hw_filter(const rtn_program_t* p, char* buf, size_t cap) {
+  return p ? copy_text(p->prog.hw_filter, buf, cap) : 0;
+}
 size_t rtn_program_conn_tree(const rtn_program_t* p, char* buf, size_t cap) {
   return p ? copy_text(p->prog.conn_tree.pprint(), buf, cap) : 0;
 }

@@ -58,6 +58,7 @@ EXPORTS = {
     "rtn_program_rust": (C.c_size_t, [C.c_void_p, C.c_char_p, C.c_size_t]),
     "rtn_program_source": (C.c_size_t, [C.c_void_p, C.c_char_p, C.c_size_t]),
     "rtn_program_deliver_table": (C.c_int32, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32]),
+    "rtn_program_hw_filter": (C.c_size_t, [C.c_void_p, C.c_char_p, C.c_size_t]),
     "rtn_program_conn_tree": (C.c_size_t, [C.c_void_p, C.c_char_p, C.c_size_t]),
     "rtn_program_conn_rust": (C.c_size_t, [C.c_void_p, C.c_char_p, C.c_size_t]),
     "rtn_program_conn_table": (C.c_int32, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32]),
@@ -197,6 +198,11 @@ class Program:
         pay = np.zeros(max(n, 1), np.uint8)
         _check(lib().rtn_program_deliver_table(self._h, subs.ctypes.data, pay.ctypes.data, max(n, 1)))
         return subs[:n], pay[:n]
+
+    @property
+    def hw_filter(self) -> str:
+        """The NIC keep/drop filter string (FilterFactory.filter_str)."""
+        return _text(lib().rtn_program_hw_filter, self._h)
 
     @property
     def conn_tree(self) -> str:

@@ -148,3 +148,15 @@ def test_both_compilers_reject(flt):
 def test_synth_alg_bytes():
     s, d = synth.cfg2(1000)
     assert synth.alg_read_bytes(s, d, 64) == 66 * 1000
+
+
+@pytest.mark.parametrize("fset", list(SETS))
+def test_hw_filter_string_matches_oracle(fset):
+    """get_hw_filter (filtergen/src/lib.rs:233-238) = PTree::to_filter_string (ptree.rs:841-870)
+    of the PacketContinue tree: the product's string equals the oracle's restatement, and it
+    re-parses (filtergen panics on an invalid HW filter). Note the reference's string lists leaf
+    paths only, so a frame that ends at an inner node with a delivery is not kept by it."""
+    hw = pc.Program.from_spec(SETS[fset]).hw_filter
+    assert hw == filterlang.PacketTree(filterlang.load_spec(SETS[fset])).to_filter_string()
+    if hw:
+        filterlang.parse_filter(hw)
