@@ -63,6 +63,13 @@ def build_library(force: bool = False) -> Path:
             f"-L{ROCM / 'lib'}", f"-Wl,-rpath,{ROCM / 'lib'}", "-lamdhip64", "-lhiprtc",
         ]
         _run(cmd)
+    # the batched offline runtime in C++ (examples/rtn_offline.cpp) on the C ABI
+    off = LIB / "rtn_offline"
+    off_src = ROOT / "examples" / "rtn_offline.cpp"
+    if force or _stale(off, [off_src, so] + hdrs):
+        _run(["g++", "-std=c++17", "-O2", "-Wall", "-D__HIP_PLATFORM_AMD__", f"-I{ROOT / 'include'}",
+              f"-I{ROCM / 'include'}", str(off_src), "-o", str(off), f"-L{LIB}", "-lretina_pc",
+              "-Wl,-rpath,$ORIGIN", f"-L{ROCM / 'lib'}", f"-Wl,-rpath,{ROCM / 'lib'}", "-lamdhip64"])
     cli = LIB / "rtnc"
     main = CSRC / "filtergen" / "rtnc_main.cpp"
     if force or _stale(cli, fg + [main] + hdrs):
