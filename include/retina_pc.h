@@ -134,6 +134,9 @@ typedef struct rtn_program_info {
   uint32_t n_conn_stmts;    /* first-packet statement sites (FilterLayer::Packet)             */
   uint32_t conn_words;      /* u64 words per first-packet statement mask                      */
   uint32_t conn_tree_size;  /* nodes of the collapsed FilterLayer::Packet tree                */
+  uint32_t n_pd_stmts;      /* packet_deliver callback sites (retina_pd.h)                     */
+  uint32_t n_pd_facts;      /* per-connection facts the packet_deliver filter reads            */
+  uint32_t pd_tree_size;    /* nodes of the collapsed FilterLayer::PacketDeliver tree          */
 } rtn_program_info_t;
 
 /* What a first-packet statement does (the host runs it with its tracked connection data). */
@@ -165,9 +168,14 @@ size_t rtn_program_hw_filter(const rtn_program_t* p, char* buf, size_t cap);
 size_t rtn_program_conn_tree(const rtn_program_t* p, char* buf, size_t cap);
 size_t rtn_program_conn_rust(const rtn_program_t* p, char* buf, size_t cap);
 int32_t rtn_program_conn_table(const rtn_program_t* p, uint32_t* sub_ids, uint8_t* kinds, uint32_t cap);
-/* A collapsed tree as JSON (layer 0 = PacketContinue, 1 = Packet): nodes with pred, actions,
+/* A collapsed tree as JSON (layer 0 = PacketContinue, 1 = Packet, 2 = PacketDeliver): nodes with pred, actions,
  * deliver/stream subscription ids, if_else and children -- for tooling and the test oracle. */
 size_t rtn_program_tree_json(const rtn_program_t* p, uint32_t layer, char* buf, size_t cap);
+/* The packet_deliver filter (retina_pd.h): JSON {"facts": [{kind: "service"|"session", pred,
+ * protocol}], "stmts": [{sub, payload, callback, loops: [[node id, fact], ...]}]} in code order,
+ * and its filtergen view. */
+size_t rtn_program_pd_json(const rtn_program_t* p, char* buf, size_t cap);
+size_t rtn_program_pd_rust(const rtn_program_t* p, char* buf, size_t cap);
 /* Compile the program's kernel for gfx950 (hiprtc; needs no GPU). Returns code-object bytes. */
 int32_t rtn_program_code_object(rtn_program_t* p, const uint8_t** data, size_t* len);
 void rtn_program_destroy(rtn_program_t* p);

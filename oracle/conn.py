@@ -189,7 +189,7 @@ def stage(pf: PacketFilter, frame: bytes, dl: int) -> tuple[int, int, list[int]]
     return h, info, fired
 
 
-__all__ = ["PacketFilter", "stage", "conn_hash", "conn_id", "creates", "Hdr", "be"]
+__all__ = ["PacketFilter", "DeliverFilter", "stage", "conn_hash", "conn_id", "creates", "Hdr", "be"]
 
 
 # ----------------------------------------------------------------------------------------------
@@ -253,3 +253,120 @@ class TableModel:
     def remove(self, keys) -> None:
         for k in keys:
             self.present.pop(k, None)
+
+
+# ----------------------------------------------------------------------------------------------
+# The generated packet_deliver (FilterLayer::PacketDeliver), run on one packet of a connection
+# that holds the PacketDeliver action (conntrack/conn/conn_info.rs:70-75).
+#
+#   filtergen/src/deliver_filter.rs:9-29     the root's deliveries first, then its children;
+#                                            add_root_pred's Ethernet wrap iff packet children
+#   filtergen/src/deliver_filter.rs:31-121   packet unary -> `if let`/`else if let` chain (first
+#                                            unary child opens it), packet binary -> if/else if by
+#                                            if_else, service -> `if matches!(conn.service(), X)`
+#                                            (else if by if_else), session binary -> a loop over
+#                                            tracked.sessions() (never part of an else chain)
+#   filtergen/src/utils.rs:251-285           update_body: children first, then the node's delivers
+#   filtergen/src/data.rs:299-317            build_packet_callback: `if let Some(p) =
+#                                            T::from_mbuf(mbuf)`; datatypes/src/packet.rs:18-29
+#                                            Payload needs offset < data_len, offset+len <= data_len
+#
+# The connection-dependent conditions are given per connection as `facts` (fact index by the
+# predicate's text, as exported in Program.pd_program()["facts"]): a service fact is 1 when the
+# connection's service is that protocol; a session fact is the number of tracked sessions that
+# satisfy the predicate, i.e. how many times the loop body runs.
+
+class DeliverFilter:
+    def __init__(self, tree: dict, subs: list, fact_preds: list[str]):
+        self.root = tree
+        self.subs = subs
+        self.fact = {p: k for k, p in enumerate(fact_preds)}
+        self.stmts: list[int] = []   # statement -> subscription id, in code order
+        self._preds: dict[int, filterlang.Pred] = {}
+        self._number(tree, True)
+
+    def _pkt(self, node: dict) -> bool:
+        return node["protocol"] in ("ethernet", "ipv4", "ipv6", "tcp", "udp")
+
+    def _pred(self, node: dict) -> filterlang.Pred:
+        if node["id"] not in self._preds:
+            dnf = filterlang.parse_filter(node["pred"])
+            assert len(dnf) == 1 and len(dnf[0]) == 1, node["pred"]
+            self._preds[node["id"]] = dnf[0][0]
+        return self._preds[node["id"]]
+
+    def _number(self, node: dict, is_root: bool = False) -> None:
+        own = []
+        if is_root:
+            for sid in sorted(node["deliver"]):
+                own.append(len(self.stmts))
+                self.stmts.append(sid)
+        for c in node["children"]:
+            self._number(c)
+        if not is_root:
+            for sid in sorted(node["deliver"]):
+                own.append(len(self.stmts))
+                self.stmts.append(sid)
+        node["_stmts"] = own
+
+    def evaluate(self, frame: bytes, dl: int, facts) -> list[int]:
+        """Statement indices in the order the callbacks run."""
+        d = bytes(frame) + bytes(max(0, 256 - len(frame)))
+        ctx = l4context(d, dl)
+        payload_ok = ctx is not None and ctx.offset < dl and ctx.offset + ctx.length <= dl
+        fired: list[int] = []
+
+        def body(node: dict):
+            for k in node["_stmts"]:
+                dts = self.subs[self.stmts[k]].datatypes
+                if "Payload" in dts and not payload_ok:
+                    continue
+                fired.append(k)
+
+        def children(node: dict, env: dict):
+            chain_taken = False
+            first_unary = True
+            for c in node["children"]:
+                pkt = self._pkt(c)
+                if not pkt and not c["unary"]:
+                    # for session in tracked.sessions() { if let X(x) = &session.data { if pred {..} } }
+                    for _ in range(int(facts[self.fact[c["pred"]]])):
+                        children(c, env)
+                        body(c)
+                    chain_taken = False
+                    continue
+                if pkt and c["unary"]:
+                    cont = not first_unary
+                    first_unary = False
+                else:
+                    cont = c["if_else"]
+                if not cont:
+                    chain_taken = False
+                if chain_taken:
+                    continue
+                env2 = env
+                if not pkt:
+                    ok = int(facts[self.fact[c["pred"]]]) != 0
+                elif c["unary"]:
+                    p = self._pred(c)
+                    h = parse(d, dl, p.proto, env[node["protocol"]])
+                    ok = h is not None
+                    if ok:
+                        env2 = dict(env)
+                        env2[p.proto] = h
+                else:
+                    p = self._pred(c)
+                    ok = eval_binary(d, env[p.proto], p)
+                if ok:
+                    chain_taken = True
+                    children(c, env2)
+                    body(c)
+
+        root = self.root
+        eth = parse(d, dl, "ethernet", None)
+        any_pkt = any(self._pkt(c) for c in root["children"])
+        if any_pkt and eth is None:
+            return []
+        body(root)
+        children(root, {"ethernet": eth})
+        return fired

@@ -136,11 +136,11 @@ struct Gen {
 
   // binary_to_tokens (utils.rs:18-249): returns {hip_expr, rust_expr}
   std::pair<std::string, std::string> binary(const Predicate& p) {
-    const bool conn = layer == FilterLayer::Packet;
+    const bool conn = layer == FilterLayer::Packet || layer == FilterLayer::PacketDeliver;
     const auto& tab = conn ? conn_fields(p.protocol) : fields(p.protocol);
     auto it = tab.find(p.field);
     if (it == tab.end()) {
-      if (conn) throw FilterError("internal: per-packet field " + p.str() + " in the first-packet filter");
+      if (conn) throw FilterError("internal: per-packet field " + p.str() + " after the packet filter");
       type_error(p, "no method named `" + p.field + "` on `" + camel(p.protocol) + "`");
     }
     const FieldDef& fd = it->second;
@@ -315,6 +315,122 @@ struct Gen {
       rust += ind(d) + "}\n";
     }
   }
+
+  // ---- FilterLayer::PacketDeliver (deliver_filter.rs) ----
+  // The body multiplies `m` (how many times the enclosing session loops run it) into per-statement
+  // counts; `f` holds the connection's facts (PdFact) and `pok` the Payload guard.
+
+  uint32_t pd_fact(const PNode& c, PdFact::Kind kind) {
+    const std::string text = c.pred.str();
+    for (size_t k = 0; k < prog.pd_facts.size(); ++k)
+      if (prog.pd_facts[k].kind == kind && prog.pd_facts[k].pred == text) return (uint32_t)k;
+    prog.pd_facts.push_back(PdFact{kind, text, c.pred.protocol});
+    return (uint32_t)prog.pd_facts.size() - 1u;
+  }
+
+  // update_body (utils.rs:251-285) at PacketDeliver: no actions (with_term_filter and
+  // with_nonterm_filter are empty there, datatypes.rs:704-721); build_packet_callback for each
+  // delivery (data.rs:299-317: `if let Some(p) = T::from_mbuf(mbuf) { cb(p, ..) }`).
+  void pd_update_body(const PNode& n, int d, const std::string& m, const std::vector<std::pair<uint32_t, uint32_t>>& loops) {
+    if (!n.actions.drop()) throw FilterError("internal: actions in the packet-deliver filter");
+    if (!n.stream.empty()) throw FilterError("internal: streaming delivery in the packet-deliver filter");
+    for (auto& dv : n.deliver) {
+      const SubscriptionSpec& spec = prog.subs.at(dv.id);
+      if (spec.level != Level::Packet) throw FilterError("internal: non-packet delivery in the packet-deliver filter");
+      std::string ty, params;
+      for (auto& dt : spec.datatypes) {
+        if (!params.empty()) params += ", ";
+        if (dt.level == Level::Packet) {
+          ty = dt.as_str;
+          params += "p";
+        } else if (dt.as_str == "FilterStr") {
+          params += "&\"" + spec.filter + "\"";
+        } else if (dt.as_str == "CoreId") {
+          params += "tracked.core_id()";  // data.rs:285-292: from the tracked data after PacketContinue
+        } else {
+          throw FilterError("Invalid datatype in packet callback: " + dt.as_str);
+        }
+      }
+      if (ty != "ZcFrame" && ty != "Payload") throw FilterError("unsupported packet datatype " + ty);
+      uint32_t k = (uint32_t)prog.pd_stmts.size();
+      prog.pd_stmts.push_back(PdStmt{DeliverStmt{(uint32_t)dv.id, ty == "Payload", spec.callback, DeliverKind::Packet}, loops});
+      std::string add = "cnt[" + std::to_string(k) + "] += " + m + ";";
+      hip += ind(d) + (ty == "Payload" ? "if (pok) { " + add + " }" : add) + "\n";
+      rust += ind(d) + "if let Some(p) = " + ty + "::from_mbuf(mbuf) { " + spec.callback + "(" + params + "); }\n";
+    }
+  }
+
+  // gen_deliver_util (deliver_filter.rs:31-121) with PacketDataFilter for packet predicates
+  // (utils.rs:298-361), ConnDataFilter::add_service_pred (utils.rs:459-486) and add_session_pred
+  // (deliver_filter.rs:123-151).
+  void pd_children(const PNode& n, int d, const std::string& m, const std::vector<std::pair<uint32_t, uint32_t>>& loops) {
+    bool first_unary = true, prev_loop = false;
+    // an `else` right after a session loop is not Rust: filtergen's output would not compile
+    auto no_else_after_loop = [&](bool is_else, const PNode& c) {
+      if (is_else && prev_loop)
+        throw FilterError("the generated packet_deliver does not compile: `else` after a session loop at " + c.pred.str());
+    };
+    for (auto& c : n.children) {
+      std::string cm = m;
+      std::vector<std::pair<uint32_t, uint32_t>> cl = loops;
+      int closes = 1;
+      if (c.pred.is_unary()) {
+        const std::string& proto = c.pred.protocol;
+        if (c.pred.on_packet()) {
+          std::string cond;
+          if (proto == "ipv4") cond = "c.v4";
+          else if (proto == "ipv6") cond = "c.v6";
+          else if (proto == "tcp") cond = "c.tcp";
+          else if (proto == "udp") cond = "c.udp";
+          else throw FilterError("internal: unexpected packet protocol " + proto);
+          no_else_after_loop(!first_unary, c);
+          hip += ind(d) + (first_unary ? "if (" : "else if (") + cond + ") {\n";
+          rust += ind(d) + (first_unary ? "if let Ok(" : "else if let Ok(") + proto + ") = parse_to::<" + camel(proto) +
+                  ">(" + n.pred.protocol + ") {\n";
+          first_unary = false;
+        } else if (c.pred.on_proto()) {
+          no_else_after_loop(c.if_else, c);
+          uint32_t k = pd_fact(c, PdFact::Service);
+          hip += ind(d) + (c.if_else ? "else if (f[" : "if (f[") + std::to_string(k) + "] != 0u) {\n";
+          std::string svc = proto;
+          if (!svc.empty()) svc[0] = (char)toupper(svc[0]);
+          rust += ind(d) + (c.if_else ? "else if " : "if ") + "matches!(conn.service(), ConnParser::" + svc + " { .. }) {\n";
+        } else {
+          throw FilterError("Unary predicate on session filter");
+        }
+      } else if (c.pred.on_packet()) {
+        no_else_after_loop(c.if_else, c);
+        auto ex = binary(c.pred);
+        hip += ind(d) + (c.if_else ? "else if " : "if ") + ex.first + " {\n";
+        rust += ind(d) + (c.if_else ? "else if " : "if ") + ex.second + " {\n";
+      } else if (c.pred.on_session()) {
+        uint32_t k = pd_fact(c, PdFact::Session);
+        cm = "m" + std::to_string(d);
+        cl.push_back({(uint32_t)c.id, k});
+        hip += ind(d) + "{\n" + ind(d + 1) + "const rtn_u32 " + cm + " = " + m + " * f[" + std::to_string(k) + "];\n" +
+               ind(d + 1) + "if (" + cm + " != 0u) {\n";
+        std::string svc = c.pred.protocol;
+        if (!svc.empty()) svc[0] = (char)toupper(svc[0]);
+        rust += ind(d) + "for session in tracked.sessions() {\n" + ind(d + 1) + "if let SessionData::" + svc + "(" +
+                c.pred.protocol + ") = &session.data {\n" + ind(d + 2) + "if /* " + c.pred.str() + " */ {\n";
+        closes = 2;
+        d += 1;
+      } else {
+        throw FilterError("Binary predicate on protocol filter");
+      }
+      prev_loop = closes == 2;
+      pd_children(c, d + 1, cm, cl);
+      pd_update_body(c, d + 1, cm, cl);
+      if (closes == 2) {
+        hip += ind(d) + "}\n" + ind(d - 1) + "}\n";
+        rust += ind(d + 1) + "}\n" + ind(d) + "}\n" + ind(d - 1) + "}\n";
+        d -= 1;
+      } else {
+        hip += ind(d) + "}\n";
+        rust += ind(d) + "}\n";
+      }
+    }
+  }
 };
 
 }  // namespace
@@ -325,9 +441,9 @@ PacketProgram compile_packet_program(const std::vector<SubscriptionSpec>& subs) 
   for (auto& s : prog.subs) s.validate_spec();
   // filtergen builds every layer's tree (filtergen/src/lib.rs:274-304) and rejects the program
   // if any of them panics (e.g. a per-packet field in a connection-level filter, ptree.rs:406-415)
-  for (FilterLayer l : {FilterLayer::Protocol, FilterLayer::Session, FilterLayer::ConnectionDeliver,
-                        FilterLayer::PacketDeliver})
+  for (FilterLayer l : {FilterLayer::Protocol, FilterLayer::Session, FilterLayer::ConnectionDeliver})
     (void)filter_subtree(l, prog.subs);
+  prog.pd_tree = filter_subtree(FilterLayer::PacketDeliver, prog.subs);
   prog.tree = filter_subtree(FilterLayer::PacketContinue, prog.subs);
   prog.conn_tree = filter_subtree(FilterLayer::Packet, prog.subs);
   // get_hw_filter (filtergen/src/lib.rs:233-238): the PacketContinue tree's paths as one filter
@@ -379,6 +495,21 @@ PacketProgram compile_packet_program(const std::vector<SubscriptionSpec>& subs) 
   prog.rust_conn_listing = "let mut result = Actions::new();\n" +
                            std::string(c_any_pkt ? "if let Ok(ethernet) = parse_to::<Ethernet>(mbuf) {\n" : "") + gc.rust +
                            (c_any_pkt ? "}\n" : "") + "result\n";
+
+  // packet_deliver (gen_deliver_filter, deliver_filter.rs:9-29): the root's deliveries, then its
+  // children; add_root_pred's Ethernet wrap (utils.rs:363-379) always parses for a tracked frame
+  Gen gd{prog, "", "", FilterLayer::PacketDeliver};
+  const PNode& droot = prog.pd_tree.root;
+  bool d_any_pkt = false;
+  for (auto& c : droot.children) d_any_pkt = d_any_pkt || c.pred.on_packet();
+  if (!droot.deliver.empty()) gd.pd_update_body(droot, 1, "1u", {});
+  gd.pd_children(droot, 1, "1u", {});
+  const bool d_wrap = !gd.rust.empty() && d_any_pkt;
+  prog.hip_pd_body =
+      "__device__ __forceinline__ void rtn_pd_filter(const rtn_cview& c, bool pok, const rtn_u32* f, rtn_u32* cnt) "
+      "{\n  (void)c; (void)pok; (void)f; (void)cnt;\n" + gd.hip + "}\n";
+  prog.rust_pd_listing = std::string(d_wrap ? "if let Ok(ethernet) = parse_to::<Ethernet>(mbuf) {\n" : "") + gd.rust +
+                         (d_wrap ? "}\n" : "");
   return prog;
 }
 

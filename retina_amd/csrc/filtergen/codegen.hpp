@@ -5,6 +5,7 @@
 //   filtergen/src/utils.rs:251-285        update_body (actions, then delivers)
 //   filtergen/src/utils.rs:298-379        PacketDataFilter::{add_unary_pred, add_binary_pred, add_root_pred}
 //   filtergen/src/data.rs:262-331         build_packet_callback (ZcFrame / Payload from_mbuf guards)
+//   filtergen/src/deliver_filter.rs:9-151 gen_deliver_filter (FilterLayer::PacketDeliver)
 #pragma once
 
 #include <string>
@@ -30,6 +31,23 @@ struct DeliverStmt {
   DeliverKind kind = DeliverKind::Packet;
 };
 
+// A condition of the PacketDeliver filter that depends on the connection, not the packet: a
+// service test `matches!(conn.service(), ConnParser::X)` (utils.rs:459-486), or a session
+// predicate looped over `tracked.sessions()` (deliver_filter.rs:123-151). The host supplies its
+// value per connection: 0/1 for a service, the number of tracked sessions satisfying it for a
+// session predicate (the body runs once per such session). One fact per distinct predicate.
+struct PdFact {
+  enum Kind : uint32_t { Service = 0, Session = 1 };
+  Kind kind;
+  std::string pred;      // the predicate as filter text
+  std::string protocol;  // its protocol (the service / session type)
+};
+
+struct PdStmt {
+  DeliverStmt d;
+  std::vector<std::pair<uint32_t, uint32_t>> loops;  // enclosing session loops (tree node id, fact), outermost first
+};
+
 struct PacketProgram {
   std::vector<SubscriptionSpec> subs;
   PTree tree{FilterLayer::PacketContinue};
@@ -46,6 +64,14 @@ struct PacketProgram {
   std::string hip_conn_body;      // __device__ rtn_conn_filter(const rtn_cview&, data, term, cm)
   std::string rust_conn_listing;
   uint32_t conn_deliver_words() const { return (uint32_t)((conn_delivers.size() + 63) / 64); }
+
+  // packet delivery for tracked connections (FilterLayer::PacketDeliver, the generated
+  // `packet_deliver`, filtergen/src/lib.rs:299-304, 357-362)
+  PTree pd_tree{FilterLayer::PacketDeliver};
+  std::vector<PdStmt> pd_stmts;
+  std::vector<PdFact> pd_facts;
+  std::string hip_pd_body;   // __device__ rtn_pd_filter(const rtn_cview&, bool payload_ok, const rtn_u32* f, rtn_u32* cnt)
+  std::string rust_pd_listing;
 };
 
 // Compile subscriptions into the PacketContinue program (and the first-packet filter). Throws FilterError on any filter

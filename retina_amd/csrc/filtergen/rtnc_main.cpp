@@ -2,6 +2,7 @@
 //   rtnc <spec.toml> [--tree] [--rust] [--hip]
 //   rtnc --filter "<filter>" [--datatype ConnRecord] ...
 //   rtnc <spec.toml> --layers      every FilterLayer's collapsed tree (filtergen/src/lib.rs:274-304)
+//   rtnc <spec.toml> --deliver     the PacketDeliver filter: tree, facts, Rust listing, HIP body
 #include <cstdio>
 #include <fstream>
 #include <iostream>
@@ -11,7 +12,7 @@
 
 int main(int argc, char** argv) {
   std::vector<rtn::SubscriptionSpec> subs;
-  bool tree = false, rust = false, hip = false, layers = false;
+  bool tree = false, rust = false, hip = false, layers = false, deliver = false;
   std::string filter;
   std::vector<std::string> dts;
   std::string spec_path;
@@ -21,11 +22,12 @@ int main(int argc, char** argv) {
     else if (a == "--rust") rust = true;
     else if (a == "--hip") hip = true;
     else if (a == "--layers") layers = true;
+    else if (a == "--deliver") deliver = true;
     else if (a == "--filter" && i + 1 < argc) filter = argv[++i];
     else if (a == "--datatype" && i + 1 < argc) dts.push_back(argv[++i]);
     else spec_path = a;
   }
-  if (!tree && !rust && !hip && !layers) tree = rust = true;
+  if (!tree && !rust && !hip && !layers && !deliver) tree = rust = true;
   try {
     if (!spec_path.empty()) {
       std::ifstream f(spec_path);
@@ -56,6 +58,13 @@ int main(int argc, char** argv) {
     if (tree) std::cout << prog.tree.pprint();
     if (rust) std::cout << prog.rust_listing;
     if (hip) std::cout << prog.hip_body;
+    if (deliver) {
+      std::cout << prog.pd_tree.pprint();
+      for (size_t k = 0; k < prog.pd_facts.size(); ++k)
+        std::cout << "fact " << k << ":" << (prog.pd_facts[k].kind == rtn::PdFact::Service ? " service " : " session ") << prog.pd_facts[k].pred
+                  << "\n";
+      std::cout << prog.rust_pd_listing << prog.hip_pd_body;
+    }
   } catch (const rtn::FilterError& e) {
     fprintf(stderr, "error: %s\n", e.what());
     return 1;

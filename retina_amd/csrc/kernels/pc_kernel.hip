@@ -764,3 +764,130 @@ __device__ __forceinline__ void rtn_lane_read(const rtn_args& a) {
 extern "C" __global__ void __launch_bounds__(256) rtn_pc_kernel(rtn_args a) RTN_BODY(RTN_MONO)
 extern "C" __global__ void __launch_bounds__(256) rtn_pc_kernel_s64(rtn_args a) RTN_BODY(RTN_S64)
 extern "C" __global__ void __launch_bounds__(256) rtn_pc_kernel_split(rtn_args a) RTN_BODY(RTN_SPLIT)
+
+// ---------------------------------------------------------------------------------------------
+// PacketDeliver filter (rtn_pd_run): the generated `packet_deliver` (filtergen/src/lib.rs:357-362,
+// deliver_filter.rs) for the forwarded frames of connections that hold the PacketDeliver action
+// (ConnInfo::update_sdata, conntrack/conn/conn_info.rs:70-75). Runs after the connection lookup:
+// a frame takes part if its connection predates the batch (RTN_CT_HIT | RTN_CT_PRIOR) and the
+// host's per-slot state says PacketDeliver is on. Packet predicates test the frame's own L4Context
+// (the deliver tree holds only connection-invariant packet fields: ptree.rs:406-415); service and
+// session predicates read the connection's facts, which the host keeps per slot.
+#ifndef RTN_PD_STMTS
+#define RTN_PD_STMTS 0
+#endif
+#ifndef RTN_PD_FACTS
+#define RTN_PD_FACTS 0
+#endif
+#define RTN_PD_S (RTN_PD_STMTS > 0 ? RTN_PD_STMTS : 1)
+#define RTN_PD_F (RTN_PD_FACTS > 0 ? RTN_PD_FACTS : 1)
+
+//@@RTN_PD_FILTER@@
+
+struct rtn_pd_args {
+  const rtn_u64* fwd_bm;
+  const rtn_l4rec* recs;
+  const unsigned char* addr6;
+  const rtn_u32* ct;           // rtn_ct_entry_t {slot, status}, indexed like recs
+  const unsigned short* dlen;
+  const rtn_u32* state;        // [state_slots][1 + RTN_PD_FACTS]: flags (bit 0: PacketDeliver), facts
+  rtn_u32 state_slots;
+  rtn_u32 n;
+  rtn_u32* counts;             // [record][RTN_PD_S]: written for delivered frames only
+  rtn_u64* pd_bm;              // [ceil(n/64)]: the frame has at least one delivery
+};
+
+// One block per 512-frame chunk, one wave per 64-frame group, one lane per frame.
+extern "C" __global__ void __launch_bounds__(512) rtn_pd_kernel(rtn_pd_args a) {
+  __shared__ rtn_u32 v6n[8];
+  const rtn_u32 lane = threadIdx.x & 63u;
+  const rtn_u32 w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const rtn_u32 ch = blockIdx.x;
+  const rtn_u32 nw = (a.n + 63u) >> 6;
+  const rtn_u32 g = ch * 8u + w;
+  const rtn_u64 lane_lt = lane ? (~0ull >> (64u - lane)) : 0ull;
+  // the chunk's bitmap words: lane j < 8 holds word j; records before this group = their popcounts
+  const rtn_u32 gj = ch * 8u + (lane & 7u);
+  const rtn_u64 wj = gj < nw ? a.fwd_bm[gj] : 0ull;
+  const rtn_u32 pop = (rtn_u32)__popcll(wj);
+  rtn_u32 pre = 0u;
+#pragma unroll
+  for (rtn_u32 j = 0; j < 8u; ++j) {
+    const rtn_u32 pj = __shfl(pop, (int)j);
+    pre += j < w ? pj : 0u;
+  }
+  const rtn_u64 word = __shfl(wj, (int)w);
+  const bool has = g < nw && ((word >> lane) & 1ull);
+  const rtn_u64 r = (rtn_u64)ch * 512u + pre + (rtn_u32)__popcll(word & lane_lt);
+  rtn_u32 rec[6] = {0u, 0u, 0u, 0u, 0u, 0u};
+  rtn_u32 slot = 0xFFFFFFFFu, st = 0u;
+  if (has) {
+    const rtn_u64* rp = reinterpret_cast<const rtn_u64*>(a.recs + r);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const rtn_u64 x = __builtin_nontemporal_load(rp + j);
+      rec[2 * j] = (rtn_u32)x;
+      rec[2 * j + 1] = (rtn_u32)(x >> 32);
+    }
+    slot = a.ct[2u * r];
+    st = a.ct[2u * r + 1u];
+  }
+  // IPv6 records are dense per chunk in addr6: rank among the chunk's IPv6 records
+  const bool v6 = has && ((rec[5] >> 7) & 1u);
+  const rtn_u64 m6 = __ballot(v6);
+  if (lane == 0u) v6n[w] = (rtn_u32)__popcll(m6);
+  __syncthreads();
+  rtn_u32 p6 = 0u;
+#pragma unroll
+  for (rtn_u32 j = 0; j < 8u; ++j) p6 += j < w ? v6n[j] : 0u;
+  const rtn_u64 r6 = (rtn_u64)ch * 512u + p6 + (rtn_u32)__popcll(m6 & lane_lt);
+
+  rtn_u32 cnt[RTN_PD_S];
+#pragma unroll
+  for (int j = 0; j < RTN_PD_S; ++j) cnt[j] = 0u;
+  bool dl = false;
+  if (has && st == (1u | 0x100u) && slot < a.state_slots) {  // RTN_CT_HIT | RTN_CT_PRIOR
+    const rtn_u32* sp = a.state + (rtn_u64)slot * (1u + RTN_PD_FACTS);
+    if (sp[0] & 1u) {
+      rtn_u32 f[RTN_PD_F];
+      f[0] = 0u;
+#pragma unroll
+      for (int j = 0; j < RTN_PD_FACTS; ++j) f[j] = sp[1 + j];
+      rtn_cview c;
+      c.v6 = v6;
+      c.v4 = !v6;
+      c.udp = (rec[5] >> 6) & 1u;
+      c.tcp = !c.udp;
+      c.src4 = rec[0];
+      c.dst4 = rec[1];
+      c.sport = rec[2] & 0xffffu;
+      c.dport = rec[2] >> 16;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        c.s6[j] = 0u;
+        c.d6[j] = 0u;
+      }
+      if (v6) {
+        const rtn_u32* ap = reinterpret_cast<const rtn_u32*>(a.addr6 + r6 * 32u);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          c.s6[j] = __builtin_bswap32(ap[j]);
+          c.d6[j] = __builtin_bswap32(ap[4 + j]);
+        }
+      }
+      // Payload::from_mbuf (datatypes/src/packet.rs:18-29): get_data_slice(offset, length)
+      const rtn_u32 dlen = a.dlen[g * 64u + lane];
+      const rtn_u32 off = ((rec[5] & 0x3fu) << 2) | 2u, len = rec[5] >> 16;
+      const bool pok = off < dlen && off + len <= dlen;
+      rtn_pd_filter(c, pok, f, cnt);
+#pragma unroll
+      for (int j = 0; j < RTN_PD_S; ++j) dl = dl || cnt[j] != 0u;
+    }
+  }
+  const rtn_u64 mb = __ballot(dl);
+  if (lane == 0u && g < nw) a.pd_bm[g] = mb;
+  if (dl) {
+#pragma unroll
+    for (int j = 0; j < RTN_PD_S; ++j) a.counts[r * RTN_PD_S + j] = cnt[j];
+  }
+}

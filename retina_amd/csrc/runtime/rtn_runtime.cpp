@@ -2,6 +2,7 @@
 // load it and launch it. See include/retina_pc.h for the contract and reference map.
 #include "retina_pc.h"
 #include "retina_ct.h"
+#include "retina_pd.h"
 
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
@@ -49,11 +50,16 @@ std::string build_source(const rtn::PacketProgram& prog) {
   const std::string marker = "//@@RTN_FILTER@@";
   size_t at = tpl.find(marker);
   std::string head = "#define RTN_DELIVER_WORDS " + std::to_string(prog.deliver_words()) + "\n" +
-                     "#define RTN_CONN_WORDS " + std::to_string(prog.conn_deliver_words()) + "\n" + env_defines();
+                     "#define RTN_CONN_WORDS " + std::to_string(prog.conn_deliver_words()) + "\n" +
+                     "#define RTN_PD_STMTS " + std::to_string(prog.pd_stmts.size()) + "\n" +
+                     "#define RTN_PD_FACTS " + std::to_string(prog.pd_facts.size()) + "\n" + env_defines();
   std::string src = head + tpl.substr(0, at) + prog.hip_body + tpl.substr(at + marker.size());
   const std::string cmarker = "//@@RTN_CONN_FILTER@@";
   size_t cat = src.find(cmarker);
-  return src.substr(0, cat) + prog.hip_conn_body + src.substr(cat + cmarker.size());
+  src = src.substr(0, cat) + prog.hip_conn_body + src.substr(cat + cmarker.size());
+  const std::string dmarker = "//@@RTN_PD_FILTER@@";
+  size_t dat = src.find(dmarker);
+  return src.substr(0, dat) + prog.hip_pd_body + src.substr(dat + dmarker.size());
 }
 
 // Kernel variants for experiments (RTN_KERNEL_DEFINES="A,B=1"); never set in production runs.
@@ -100,6 +106,27 @@ std::string node_json(const rtn::PNode& n) {
   }
   o += "],\"children\":[";
   for (size_t k = 0; k < n.children.size(); ++k) o += (k ? "," : "") + node_json(n.children[k]);
+  return o + "]}";
+}
+
+// The PacketDeliver program for the host: its facts (what the host computes per connection) and
+// its statements in code order, each with the session loops around it.
+std::string pd_json(const rtn::PacketProgram& prog) {
+  std::string o = "{\"facts\":[";
+  for (size_t k = 0; k < prog.pd_facts.size(); ++k) {
+    const auto& f = prog.pd_facts[k];
+    o += std::string(k ? "," : "") + "{\"kind\":" + (f.kind == rtn::PdFact::Service ? "\"service\"" : "\"session\"") +
+         ",\"pred\":" + json_str(f.pred) + ",\"protocol\":" + json_str(f.protocol) + "}";
+  }
+  o += "],\"stmts\":[";
+  for (size_t k = 0; k < prog.pd_stmts.size(); ++k) {
+    const auto& st = prog.pd_stmts[k];
+    o += std::string(k ? "," : "") + "{\"sub\":" + std::to_string(st.d.sub_id) +
+         ",\"payload\":" + (st.d.payload ? "true" : "false") + ",\"callback\":" + json_str(st.d.callback) + ",\"loops\":[";
+    for (size_t j = 0; j < st.loops.size(); ++j)
+      o += std::string(j ? "," : "") + "[" + std::to_string(st.loops[j].first) + "," + std::to_string(st.loops[j].second) + "]";
+    o += "]}";
+  }
   return o + "]}";
 }
 
@@ -169,6 +196,20 @@ struct KArgs {
   uint64_t* conn_dlv;
 };
 
+// must match struct rtn_pd_args in pc_kernel.hip
+struct PdArgs {
+  const uint64_t* fwd_bm;
+  const rtn_l4ctx_t* recs;
+  const uint8_t* addr6;
+  const rtn_ct_entry_t* ct;
+  const uint16_t* dlen;
+  const uint32_t* state;
+  uint32_t state_slots;
+  uint32_t n;
+  uint32_t* counts;
+  uint64_t* pd_bm;
+};
+
 }  // namespace
 
 struct rtn_program {
@@ -185,6 +226,7 @@ struct rtn_pc {
   hipFunction_t fn = nullptr;        // rtn_pc_kernel: monolithic slots, any stride (multiple of 64)
   hipFunction_t fn_s64 = nullptr;    // rtn_pc_kernel_s64: 64-byte slots
   hipFunction_t fn_split = nullptr;  // rtn_pc_kernel_split: 64-byte slots + ext
+  hipFunction_t fn_pd = nullptr;     // rtn_pd_kernel: the PacketDeliver filter (rtn_pd_run)
   uint32_t blocks = 0;
   uint32_t* scratch_counters = nullptr;  // used when the caller passes no counters
 };
@@ -252,6 +294,9 @@ int32_t rtn_program_info(const rtn_program_t* p, rtn_program_info_t* info) {
   info->n_conn_stmts = (uint32_t)p->prog.conn_delivers.size();
   info->conn_words = p->prog.conn_deliver_words();
   info->conn_tree_size = (uint32_t)p->prog.conn_tree.size;
+  info->n_pd_stmts = (uint32_t)p->prog.pd_stmts.size();
+  info->n_pd_facts = (uint32_t)p->prog.pd_facts.size();
+  info->pd_tree_size = (uint32_t)p->prog.pd_tree.size;
   return RTN_OK;
 }
 
@@ -265,8 +310,15 @@ size_t rtn_program_conn_rust(const rtn_program_t* p, char* buf, size_t cap) {
   return p ? copy_text(p->prog.rust_conn_listing, buf, cap) : 0;
 }
 size_t rtn_program_tree_json(const rtn_program_t* p, uint32_t layer, char* buf, size_t cap) {
-  if (!p || layer > 1) return 0;
-  return copy_text(node_json(layer == 0 ? p->prog.tree.root : p->prog.conn_tree.root), buf, cap);
+  if (!p || layer > 2) return 0;
+  const rtn::PNode& r = layer == 0 ? p->prog.tree.root : layer == 1 ? p->prog.conn_tree.root : p->prog.pd_tree.root;
+  return copy_text(node_json(r), buf, cap);
+}
+size_t rtn_program_pd_json(const rtn_program_t* p, char* buf, size_t cap) {
+  return p ? copy_text(pd_json(p->prog), buf, cap) : 0;
+}
+size_t rtn_program_pd_rust(const rtn_program_t* p, char* buf, size_t cap) {
+  return p ? copy_text(p->prog.rust_pd_listing, buf, cap) : 0;
 }
 
 int32_t rtn_program_conn_table(const rtn_program_t* p, uint32_t* sub_ids, uint8_t* kinds, uint32_t cap) {
@@ -331,6 +383,8 @@ int32_t rtn_pc_create_from_program(rtn_program_t* p, int device, rtn_pc_t** out)
   e = hipModuleGetFunction(&pc->fn_s64, pc->module, "rtn_pc_kernel_s64");
   if (e != hipSuccess) return fail(RTN_EDEVICE, std::string("hipModuleGetFunction: ") + hipGetErrorString(e));
   e = hipModuleGetFunction(&pc->fn_split, pc->module, "rtn_pc_kernel_split");
+  if (e != hipSuccess) return fail(RTN_EDEVICE, std::string("hipModuleGetFunction: ") + hipGetErrorString(e));
+  e = hipModuleGetFunction(&pc->fn_pd, pc->module, "rtn_pd_kernel");
   if (e != hipSuccess) return fail(RTN_EDEVICE, std::string("hipModuleGetFunction: ") + hipGetErrorString(e));
   e = hipMalloc(&pc->scratch_counters, 16);
   if (e != hipSuccess) return fail(RTN_EDEVICE, std::string("hipMalloc: ") + hipGetErrorString(e));
@@ -409,6 +463,36 @@ int32_t rtn_pc_run(rtn_pc_t* pc, const rtn_batch_t* in, rtn_pc_out_t* out, void*
   return RTN_OK;
 }
 
+int32_t rtn_pd_run(rtn_pc_t* pc, const rtn_pc_out_t* out, const rtn_ct_entry_t* ct, const uint16_t* data_len,
+                   uint32_t n, const uint32_t* state, uint32_t state_slots, uint32_t* counts, uint64_t* pd_bitmap,
+                   void* stream) {
+  if (!pc || !out || !ct || !data_len || !pd_bitmap) return fail(RTN_EINVAL, "null argument");
+  if (n == 0) return RTN_OK;
+  if (!out->fwd_bitmap || !out->l4 || !out->addr6) return fail(RTN_EINVAL, "fwd_bitmap, l4 and addr6 required");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (pc->program->prog.pd_stmts.empty()) {  // no packet-level subscription: nothing is delivered
+    hipError_t e = hipMemsetAsync(pd_bitmap, 0, rtn_out_bitmap_bytes(n), s);
+    return e == hipSuccess ? RTN_OK : fail(RTN_EDEVICE, std::string("hipMemsetAsync: ") + hipGetErrorString(e));
+  }
+  if (!state || !counts) return fail(RTN_EINVAL, "state and counts required");
+  PdArgs a;
+  a.fwd_bm = out->fwd_bitmap;
+  a.recs = out->l4;
+  a.addr6 = out->addr6;
+  a.ct = ct;
+  a.dlen = data_len;
+  a.state = state;
+  a.state_slots = state_slots;
+  a.n = n;
+  a.counts = counts;
+  a.pd_bm = pd_bitmap;
+  void* params[] = {&a};
+  const uint32_t chunks = (n + RTN_CHUNK_FRAMES - 1u) / RTN_CHUNK_FRAMES;
+  hipError_t e = hipModuleLaunchKernel(pc->fn_pd, chunks, 1, 1, RTN_CHUNK_FRAMES, 1, 1, 0, s, params, nullptr);
+  if (e != hipSuccess) return fail(RTN_EDEVICE, std::string("hipModuleLaunchKernel: ") + hipGetErrorString(e));
+  return RTN_OK;
+}
+
 int32_t rtn_pc_destroy(rtn_pc_t* pc) {
   if (!pc) return RTN_OK;
   if (pc->scratch_counters) (void)hipFree(pc->scratch_counters);
@@ -429,6 +513,9 @@ size_t rtn_out_dlv_bytes(uint32_t n, uint32_t deliver_words) {
 static_assert(sizeof(rtn_conn_t) == 8, "rtn_conn_t is 8 bytes");
 size_t rtn_out_conn_bytes(uint32_t n) { return chunked(n) * sizeof(rtn_conn_t); }
 size_t rtn_out_conn_dlv_bytes(uint32_t n, uint32_t conn_words) { return chunked(n) * conn_words * 8u; }
+size_t rtn_out_pd_counts_bytes(uint32_t n, uint32_t n_pd_stmts) {
+  return chunked(n) * (n_pd_stmts ? n_pd_stmts : 1u) * sizeof(uint32_t);
+}
 
 
 }  // extern "C"

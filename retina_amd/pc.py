@@ -46,7 +46,8 @@ class _PcapStats(C.Structure):
 class _Info(C.Structure):
     _fields_ = [("n_subscriptions", C.c_uint32), ("n_deliver_stmts", C.c_uint32),
                 ("deliver_words", C.c_uint32), ("tree_size", C.c_uint32), ("n_conn_stmts", C.c_uint32),
-                ("conn_words", C.c_uint32), ("conn_tree_size", C.c_uint32)]
+                ("conn_words", C.c_uint32), ("conn_tree_size", C.c_uint32), ("n_pd_stmts", C.c_uint32),
+                ("n_pd_facts", C.c_uint32), ("pd_tree_size", C.c_uint32)]
 
 
 EXPORTS = {
@@ -63,6 +64,8 @@ EXPORTS = {
     "rtn_program_conn_rust": (C.c_size_t, [C.c_void_p, C.c_char_p, C.c_size_t]),
     "rtn_program_conn_table": (C.c_int32, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32]),
     "rtn_program_tree_json": (C.c_size_t, [C.c_void_p, C.c_uint32, C.c_char_p, C.c_size_t]),
+    "rtn_program_pd_json": (C.c_size_t, [C.c_void_p, C.c_char_p, C.c_size_t]),
+    "rtn_program_pd_rust": (C.c_size_t, [C.c_void_p, C.c_char_p, C.c_size_t]),
     "rtn_program_code_object": (C.c_int32, [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]),
     "rtn_program_destroy": (None, [C.c_void_p]),
     "rtn_pc_create": (C.c_int32, [C.c_char_p, C.c_size_t, C.c_int, C.POINTER(C.c_void_p)]),
@@ -85,6 +88,10 @@ EXPORTS = {
     "rtn_ct_stats": (C.c_int32, [C.c_void_p, C.c_void_p]),
     "rtn_ct_table": (C.c_void_p, [C.c_void_p]),
     "rtn_out_ct_bytes": (C.c_size_t, [C.c_uint32]),
+    # include/retina_pd.h
+    "rtn_pd_run": (C.c_int32, [C.c_void_p, C.POINTER(_Out), C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p,
+                               C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "rtn_out_pd_counts_bytes": (C.c_size_t, [C.c_uint32, C.c_uint32]),
     # include/retina_ingest.h
     "rtn_pcap_open": (C.c_int32, [C.c_char_p, C.c_uint32, C.POINTER(C.c_void_p)]),
     "rtn_pcap_next_batch": (C.c_int32, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint32,
@@ -221,8 +228,19 @@ class Program:
         _check(lib().rtn_program_conn_table(self._h, subs.ctypes.data, kinds.ctypes.data, max(n, 1)))
         return subs[:n], kinds[:n]
 
+    @property
+    def pd_rust(self) -> str:
+        """The generated packet_deliver as filtergen would emit it (FilterLayer::PacketDeliver)."""
+        return _text(lib().rtn_program_pd_rust, self._h)
+
+    def pd_program(self) -> dict:
+        """The packet_deliver filter's facts and statements (include/retina_pd.h)."""
+        import json
+
+        return json.loads(_text(lib().rtn_program_pd_json, self._h))
+
     def tree_json(self, layer: int) -> dict:
-        """Collapsed tree of layer 0 (PacketContinue) or 1 (Packet) as nested dicts."""
+        """Collapsed tree of layer 0 (PacketContinue), 1 (Packet) or 2 (PacketDeliver) as nested dicts."""
         import json
 
         L = lib()
@@ -370,6 +388,78 @@ class PacketContinue:
         _check(lib().rtn_pc_run(self._h, C.byref(b), C.byref(o), C.c_void_p(s.cuda_stream)))
         out.n = n
         return out
+
+
+PD_ACTIVE = 1  # RTN_PD_ACTIVE (include/retina_pd.h)
+
+
+def pd_run(pc: "PacketContinue", pc_out: PCOutputs, ct_entries, data_len, state, counts=None, bitmap=None,
+           stream=None):
+    """rtn_pd_run: the packet_deliver filter over a batch, after ConnTable.process. `state` is the
+    device uint32 [slots][1 + n_pd_facts] per-connection table. Returns (counts, bitmap) device
+    tensors: counts [record][n_pd_stmts] uint32 (valid where the bitmap is set)."""
+    import torch
+
+    if pc_out.addr6 is None:
+        raise RetinaError(-22, "pd_run needs outputs allocated with addr6=True")
+    n = pc_out.n
+    L = lib()
+    dev = torch.device("cuda", pc.device)
+    ns = pc.program.info["n_pd_stmts"]
+    nf = pc.program.info["n_pd_facts"]
+    if state.numel() % (1 + nf) != 0:
+        raise RetinaError(-22, f"state must hold rows of 1 + {nf} uint32")
+    if counts is None:
+        counts = torch.empty(L.rtn_out_pd_counts_bytes(max(n, 1), ns) // 4, dtype=torch.int32, device=dev)
+    if bitmap is None:
+        bitmap = torch.empty(L.rtn_out_bitmap_bytes(max(n, 1)), dtype=torch.uint8, device=dev)
+    o = _out_struct(pc_out)
+    s = stream if stream is not None else torch.cuda.current_stream(pc.device)
+    _check(L.rtn_pd_run(pc._h, C.byref(o), C.c_void_p(ct_entries.data_ptr()), C.c_void_p(data_len.data_ptr()), n,
+                        C.c_void_p(state.data_ptr()), int(state.numel() // (1 + nf)), C.c_void_p(counts.data_ptr()),
+                        C.c_void_p(bitmap.data_ptr()), C.c_void_p(s.cuda_stream)))
+    return counts, bitmap
+
+
+def decode_pd(counts, bitmap, pc_out: PCOutputs, n_stmts: int) -> tuple[np.ndarray, np.ndarray]:
+    """(frame indices with a delivery, their per-statement counts) in frame order."""
+    n = pc_out.n
+    fwd_bm = pc_out.fwd_bitmap.cpu().numpy().view(np.uint64)
+    fwd = np.nonzero(np.unpackbits(fwd_bm.view(np.uint8), bitorder="little")[:n])[0]
+    rec = _rank_index(fwd)
+    bm = bitmap.cpu().numpy().view(np.uint64)
+    hit = np.unpackbits(bm.view(np.uint8), bitorder="little")[:n].astype(bool)
+    sel = hit[fwd]
+    c = counts.cpu().numpy().view(np.uint32).reshape(-1, max(n_stmts, 1))[:, :n_stmts]
+    return fwd[sel], c[rec[sel]]
+
+
+def pd_replay(pd: dict, counts_row, facts_row) -> list[int]:
+    """The callback sequence (statement indices) the reference runs for one frame. A session loop
+    runs its body once per matching session (deliver_filter.rs:123-151), i.e. facts_row[fact]
+    times, so the statements of one loop body repeat as a block; a statement fires in a pass iff
+    its count is non-zero (its packet and service conditions do not depend on the session)."""
+    stmts = pd["stmts"]
+
+    def rec(idx: list[int], depth: int) -> list[int]:
+        out: list[int] = []
+        i = 0
+        while i < len(idx):
+            loops = stmts[idx[i]]["loops"]
+            if len(loops) == depth:
+                if counts_row[idx[i]]:
+                    out.append(idx[i])
+                i += 1
+                continue
+            node, fact = loops[depth]
+            j = i
+            while j < len(idx) and len(stmts[idx[j]]["loops"]) > depth and stmts[idx[j]]["loops"][depth][0] == node:
+                j += 1
+            out += rec(idx[i:j], depth + 1) * int(facts_row[fact])
+            i = j
+        return out
+
+    return rec(list(range(len(stmts))), 0)
 
 
 def _out_struct(out: PCOutputs) -> _Out:

@@ -51,7 +51,8 @@ def test_error_codes_and_messages():
 def test_program_text_outputs():
     p = pc.Program.from_spec(SETS["cfg2"])
     assert p.info == {"n_subscriptions": 1, "n_deliver_stmts": 0, "deliver_words": 0, "tree_size": 7,
-                      "n_conn_stmts": 0, "conn_words": 0, "conn_tree_size": 3}
+                      "n_conn_stmts": 0, "conn_words": 0, "conn_tree_size": 3, "n_pd_stmts": 0,
+                      "n_pd_facts": 0, "pd_tree_size": 1}
     assert "tcp.dst_port = 80" in p.tree
     assert "if tcp.dst_port() == 80 {" in p.rust
     assert "rtn_pc_kernel" in p.source and "RTN_DELIVER_WORDS 0" in p.source
