@@ -168,6 +168,63 @@ def e2e_rate(ctx, slab: np.ndarray, dlen: np.ndarray, stride: int, dev) -> dict:
                     "2 streams; PCIe-bound"}
 
 
+# Packet-level subscriptions that match at the protocol/session layer: their packets are
+# delivered by packet_deliver (include/retina_pd.h) once the connection holds PacketDeliver.
+PD_SPEC = """
+[[subscriptions]]
+filter = "tls"
+datatypes = ["ZcFrame"]
+callback = "tls_cb"
+
+[[subscriptions]]
+filter = "tcp.port = 80 and http.user_agent ~ 'curl'"
+datatypes = ["Payload"]
+callback = "http_cb"
+
+[[subscriptions]]
+filter = "ipv4.addr = 10.0.0.0/8 and tls.sni ~ 'x'"
+datatypes = ["ZcFrame", "FilterStr"]
+callback = "t2_cb"
+"""
+
+
+def pd_rate(cfg, d_slab, stride, d_dlen, n, d_ext, device, stream, steps) -> dict:
+    """Side measurement: rtn_pd_run over the batch with every frame's connection established
+    before the batch and holding PacketDeliver (the worst case: every forwarded frame evaluates
+    the tree and gathers its connection's state)."""
+    import torch
+
+    from retina_amd import pc
+
+    prog = pc.Program.from_spec(PD_SPEC)
+    ctx = pc.PacketContinue(prog, device)
+    out = ctx.alloc_outputs(n, addr6=True, counters=False, conn=True)
+    ctx.run(d_slab, stride, d_dlen, n, out, stream=stream, ext=d_ext)
+    ct = pc.ConnTable(device, 26, 1 << 26)
+    ent = ct.process(out, stream=stream)
+    ct.process(out, out=ent, stream=stream)  # every opener now predates the batch
+    nf = prog.info["n_pd_facts"]
+    g = torch.Generator(device="cpu").manual_seed(5)
+    state = torch.randint(0, 3, (ct.capacity, 1 + nf), generator=g, dtype=torch.int32)
+    state[:, 0] = pc.PD_ACTIVE
+    state = state.to(torch.device("cuda", device))
+    counts, bm = pc.pd_run(ctx, out, ent, d_dlen, state, stream=stream)
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(steps):
+        pc.pd_run(ctx, out, ent, d_dlen, state, counts, bm, stream=stream)
+    e1.record(stream)
+    torch.cuda.synchronize(device)
+    ms = e0.elapsed_time(e1) / steps
+    fwd = int(np.unpackbits(out.fwd_bitmap.cpu().numpy()).sum())
+    delivered = int(np.unpackbits(bm.cpu().numpy()).sum())
+    del ct, state, out, counts, bm, ctx
+    torch.cuda.empty_cache()
+    return {"ms": round(ms, 4), "mpps": round(n / ms / 1e3, 1), "forwarded": fwd, "frames_with_delivery": delivered, "stmts": prog.info["n_pd_stmts"], "facts": nf,
+            "tree_size": prog.info["pd_tree_size"]}
+
+
 def counters_fwd_hint(out) -> int:
     """Forwarded frames of a finished run (popcount of its fwd bitmap)."""
     import numpy as np_
@@ -293,6 +350,8 @@ def main() -> None:
         ctms = k0.elapsed_time(k1) / args.steps
         ct_stats = ct.stats()
         del ct
+        pd_stage = pd_rate(cfg, d_slab, run_stride, d_dlen, n, d_ext, local, stream, args.steps) \
+            if cfg == "cfg2" else None
         conn_stage = {"kernel_ms": round(cms, 4), "mpps": round(n / cms / 1e3, 1),
                       "vs_filter_only": round(kern_ms / cms, 3),
                       "first_packet_tree_size": prog.info["conn_tree_size"],
@@ -300,6 +359,7 @@ def main() -> None:
                                     "first_pass_ms": round(ct_first, 4), "opened_first_pass": ct_stats["live"],
                                     "forwarded_per_s_M": round(counters_fwd_hint(cout) / ctms / 1e3, 1),
                                     "table_slots": ct_stats["capacity"], "live": ct_stats["live"]},
+                      "packet_deliver": pd_stage,
                       "note": "same step + rtn_conn_t (8 B) per forwarded frame: ConnId hash/orientation, "
                               "creates bit, first-packet packet_filter actions"}
         del cout

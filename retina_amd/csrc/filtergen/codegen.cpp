@@ -431,6 +431,61 @@ struct Gen {
       }
     }
   }
+  // The same tree as straight-line HIP: every node's reach flag and multiplier is computed with
+  // selects, and each statement's count is assigned once. (Branchy code let the compiler sink the
+  // `cnt[k] += m` of sibling branches into one store with a computed index, which moves the
+  // counters to scratch memory.) Statement and fact numbering follow pd_children / pd_update_body.
+  uint32_t flat_stmt = 0;
+  void pd_flat_body(const PNode& n, const std::string& R, const std::string& M) {
+    for (auto& dv : n.deliver) {
+      uint32_t k = flat_stmt++;
+      if (k >= prog.pd_stmts.size() || prog.pd_stmts[k].d.sub_id != (uint32_t)dv.id)
+        throw FilterError("internal: packet-deliver statement order");
+      std::string reach = prog.pd_stmts[k].d.payload ? "(" + R + " && pok)" : R;
+      hip += "  cnt[" + std::to_string(k) + "] = " + reach + " ? " + M + " : 0u;\n";
+    }
+  }
+  void pd_flat(const PNode& n, const std::string& R, const std::string& M) {
+    bool first_unary = true;
+    std::string T;  // the open if-chain's "some branch taken" flag
+    for (auto& c : n.children) {
+      const std::string id = std::to_string(c.id);
+      std::string rc = "r" + id, mc = M;
+      if (!c.pred.is_unary() && c.pred.on_session()) {
+        uint32_t k = pd_fact(c, PdFact::Session);
+        mc = "m" + id;
+        hip += "  const rtn_u32 " + mc + " = " + M + " * f[" + std::to_string(k) + "];\n";
+        hip += "  const bool " + rc + " = " + R + " && " + mc + " != 0u;\n";
+        T.clear();
+      } else {
+        std::string cond;
+        bool is_else;
+        if (c.pred.is_unary() && c.pred.on_packet()) {
+          const std::string& proto = c.pred.protocol;
+          cond = proto == "ipv4" ? "c.v4" : proto == "ipv6" ? "c.v6" : proto == "tcp" ? "c.tcp" : "c.udp";
+          is_else = !first_unary;
+          first_unary = false;
+        } else if (c.pred.is_unary()) {
+          cond = "(f[" + std::to_string(pd_fact(c, PdFact::Service)) + "] != 0u)";
+          is_else = c.if_else;
+        } else {
+          cond = binary(c.pred).first;
+          is_else = c.if_else;
+        }
+        hip += "  const bool k" + id + " = " + cond + ";\n";
+        if (!is_else || T.empty()) {
+          T = "t" + id;
+          hip += "  bool " + T + " = k" + id + ";\n";
+          hip += "  const bool " + rc + " = " + R + " && k" + id + ";\n";
+        } else {
+          hip += "  const bool " + rc + " = " + R + " && !" + T + " && k" + id + ";\n";
+          hip += "  " + T + " = " + T + " || k" + id + ";\n";
+        }
+      }
+      pd_flat(c, rc, mc);
+      pd_flat_body(c, rc, mc);
+    }
+  }
 };
 
 }  // namespace
@@ -504,6 +559,10 @@ PacketProgram compile_packet_program(const std::vector<SubscriptionSpec>& subs) 
   for (auto& c : droot.children) d_any_pkt = d_any_pkt || c.pred.on_packet();
   if (!droot.deliver.empty()) gd.pd_update_body(droot, 1, "1u", {});
   gd.pd_children(droot, 1, "1u", {});
+  gd.hip.clear();
+  gd.pd_flat_body(droot, "true", "1u");
+  gd.pd_flat(droot, "true", "1u");
+  if (gd.flat_stmt != prog.pd_stmts.size()) throw FilterError("internal: packet-deliver statement count");
   const bool d_wrap = !gd.rust.empty() && d_any_pkt;
   prog.hip_pd_body =
       "__device__ __forceinline__ void rtn_pd_filter(const rtn_cview& c, bool pok, const rtn_u32* f, rtn_u32* cnt) "

@@ -797,71 +797,106 @@ struct rtn_pd_args {
   rtn_u64* pd_bm;              // [ceil(n/64)]: the frame has at least one delivery
 };
 
-// One block per 512-frame chunk, one wave per 64-frame group, one lane per frame.
-extern "C" __global__ void __launch_bounds__(512) rtn_pd_kernel(rtn_pd_args a) {
+#ifndef RTN_PD_GPW
+// groups (64 frames) per wave (1, 2, 4 and 8 measured within 3 % on cfg2: 0.40-0.41 ms; 1 is
+// the fastest)
+#define RTN_PD_GPW 1u
+#endif
+#define RTN_PD_THREADS (512u / RTN_PD_GPW)
+
+// One block per 512-frame chunk, RTN_PD_GPW 64-frame groups per wave, one lane per frame of each.
+extern "C" __global__ void __launch_bounds__(RTN_PD_THREADS) rtn_pd_kernel(rtn_pd_args a) {
+  constexpr rtn_u32 G = RTN_PD_GPW;
   __shared__ rtn_u32 v6n[8];
   const rtn_u32 lane = threadIdx.x & 63u;
   const rtn_u32 w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const rtn_u32 ch = blockIdx.x;
   const rtn_u32 nw = (a.n + 63u) >> 6;
-  const rtn_u32 g = ch * 8u + w;
   const rtn_u64 lane_lt = lane ? (~0ull >> (64u - lane)) : 0ull;
-  // the chunk's bitmap words: lane j < 8 holds word j; records before this group = their popcounts
+  // the chunk's bitmap words: lane j < 8 holds word j; pre[j] = records before group j
   const rtn_u32 gj = ch * 8u + (lane & 7u);
   const rtn_u64 wj = gj < nw ? a.fwd_bm[gj] : 0ull;
   const rtn_u32 pop = (rtn_u32)__popcll(wj);
-  rtn_u32 pre = 0u;
+  // (q = w * G + u is not a compile-time index: accumulate per group instead of indexing an array)
+  rtn_u32 pre[G];
+#pragma unroll
+  for (rtn_u32 u = 0; u < G; ++u) pre[u] = 0u;
 #pragma unroll
   for (rtn_u32 j = 0; j < 8u; ++j) {
     const rtn_u32 pj = __shfl(pop, (int)j);
-    pre += j < w ? pj : 0u;
-  }
-  const rtn_u64 word = __shfl(wj, (int)w);
-  const bool has = g < nw && ((word >> lane) & 1ull);
-  const rtn_u64 r = (rtn_u64)ch * 512u + pre + (rtn_u32)__popcll(word & lane_lt);
-  rtn_u32 rec[6] = {0u, 0u, 0u, 0u, 0u, 0u};
-  rtn_u32 slot = 0xFFFFFFFFu, st = 0u;
-  if (has) {
-    const rtn_u64* rp = reinterpret_cast<const rtn_u64*>(a.recs + r);
 #pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      const rtn_u64 x = __builtin_nontemporal_load(rp + j);
-      rec[2 * j] = (rtn_u32)x;
-      rec[2 * j + 1] = (rtn_u32)(x >> 32);
+    for (rtn_u32 u = 0; u < G; ++u) pre[u] += j < w * G + u ? pj : 0u;
+  }
+  bool has[G];
+  rtn_u64 r[G];
+  rtn_u32 rec[G][6], slot[G], st[G];
+#pragma unroll
+  for (rtn_u32 u = 0; u < G; ++u) {
+    const rtn_u32 q = w * G + u;
+    const rtn_u64 word = __shfl(wj, (int)q);
+    has[u] = ch * 8u + q < nw && ((word >> lane) & 1ull);
+    r[u] = (rtn_u64)ch * 512u + pre[u] + (rtn_u32)__popcll(word & lane_lt);
+#pragma unroll
+    for (int j = 0; j < 6; ++j) rec[u][j] = 0u;
+    slot[u] = 0xFFFFFFFFu;
+    st[u] = 0u;
+    if (has[u]) {
+      const rtn_u64* rp = reinterpret_cast<const rtn_u64*>(a.recs + r[u]);
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const rtn_u64 x = __builtin_nontemporal_load(rp + j);
+        rec[u][2 * j] = (rtn_u32)x;
+        rec[u][2 * j + 1] = (rtn_u32)(x >> 32);
+      }
+      const rtn_u64 e = __builtin_nontemporal_load(reinterpret_cast<const rtn_u64*>(a.ct) + r[u]);
+      slot[u] = (rtn_u32)e;
+      st[u] = (rtn_u32)(e >> 32);
     }
-    slot = a.ct[2u * r];
-    st = a.ct[2u * r + 1u];
+  }
+  // the connection's state row: flags and facts in one go (RTN_CT_HIT | RTN_CT_PRIOR only)
+  bool on[G];
+  rtn_u32 sv[G][1 + RTN_PD_F];
+#pragma unroll
+  for (rtn_u32 u = 0; u < G; ++u) {
+    on[u] = has[u] && st[u] == (1u | 0x100u) && slot[u] < a.state_slots;
+#pragma unroll
+    for (int j = 0; j <= RTN_PD_F; ++j) sv[u][j] = 0u;
+    if (on[u]) {
+      const rtn_u32* sp = a.state + (rtn_u64)slot[u] * (1u + RTN_PD_FACTS);
+#pragma unroll
+      for (int j = 0; j <= RTN_PD_FACTS; ++j) sv[u][j] = sp[j];
+    }
   }
   // IPv6 records are dense per chunk in addr6: rank among the chunk's IPv6 records
-  const bool v6 = has && ((rec[5] >> 7) & 1u);
-  const rtn_u64 m6 = __ballot(v6);
-  if (lane == 0u) v6n[w] = (rtn_u32)__popcll(m6);
+  rtn_u64 m6[G];
+#pragma unroll
+  for (rtn_u32 u = 0; u < G; ++u) {
+    m6[u] = __ballot(has[u] && ((rec[u][5] >> 7) & 1u));
+    if (lane == 0u) v6n[w * G + u] = (rtn_u32)__popcll(m6[u]);
+  }
   __syncthreads();
-  rtn_u32 p6 = 0u;
 #pragma unroll
-  for (rtn_u32 j = 0; j < 8u; ++j) p6 += j < w ? v6n[j] : 0u;
-  const rtn_u64 r6 = (rtn_u64)ch * 512u + p6 + (rtn_u32)__popcll(m6 & lane_lt);
-
-  rtn_u32 cnt[RTN_PD_S];
+  for (rtn_u32 u = 0; u < G; ++u) {
+    const rtn_u32 q = w * G + u;
+    const bool v6 = (m6[u] >> lane) & 1ull;
+    rtn_u32 cnt[RTN_PD_S];
 #pragma unroll
-  for (int j = 0; j < RTN_PD_S; ++j) cnt[j] = 0u;
-  bool dl = false;
-  if (has && st == (1u | 0x100u) && slot < a.state_slots) {  // RTN_CT_HIT | RTN_CT_PRIOR
-    const rtn_u32* sp = a.state + (rtn_u64)slot * (1u + RTN_PD_FACTS);
-    if (sp[0] & 1u) {
-      rtn_u32 f[RTN_PD_F];
-      f[0] = 0u;
+    for (int j = 0; j < RTN_PD_S; ++j) cnt[j] = 0u;
+    bool dl = false;
+    if (on[u] && (sv[u][0] & 1u)) {
+      rtn_u32 p6 = 0u;
 #pragma unroll
-      for (int j = 0; j < RTN_PD_FACTS; ++j) f[j] = sp[1 + j];
+      for (rtn_u32 j = 0; j < 8u; ++j) p6 += j < q ? v6n[j] : 0u;
+      const rtn_u64 r6 = (rtn_u64)ch * 512u + p6 + (rtn_u32)__popcll(m6[u] & lane_lt);
       rtn_cview c;
       c.v6 = v6;
       c.v4 = !v6;
-      c.udp = (rec[5] >> 6) & 1u;
+      c.udp = (rec[u][5] >> 6) & 1u;
       c.tcp = !c.udp;
-      c.src4 = rec[0];
-      c.dst4 = rec[1];
-      c.sport = rec[2] & 0xffffu;
-      c.dport = rec[2] >> 16;
+      c.src4 = rec[u][0];
+      c.dst4 = rec[u][1];
+      c.sport = rec[u][2] & 0xffffu;
+      c.dport = rec[u][2] >> 16;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         c.s6[j] = 0u;
@@ -876,18 +911,18 @@ extern "C" __global__ void __launch_bounds__(512) rtn_pd_kernel(rtn_pd_args a) {
         }
       }
       // Payload::from_mbuf (datatypes/src/packet.rs:18-29): get_data_slice(offset, length)
-      const rtn_u32 dlen = a.dlen[g * 64u + lane];
-      const rtn_u32 off = ((rec[5] & 0x3fu) << 2) | 2u, len = rec[5] >> 16;
+      const rtn_u32 dlen = a.dlen[(ch * 8u + q) * 64u + lane];
+      const rtn_u32 off = ((rec[u][5] & 0x3fu) << 2) | 2u, len = rec[u][5] >> 16;
       const bool pok = off < dlen && off + len <= dlen;
-      rtn_pd_filter(c, pok, f, cnt);
+      rtn_pd_filter(c, pok, &sv[u][1], cnt);
 #pragma unroll
       for (int j = 0; j < RTN_PD_S; ++j) dl = dl || cnt[j] != 0u;
     }
-  }
-  const rtn_u64 mb = __ballot(dl);
-  if (lane == 0u && g < nw) a.pd_bm[g] = mb;
-  if (dl) {
+    const rtn_u64 mb = __ballot(dl);
+    if (lane == 0u && ch * 8u + q < nw) a.pd_bm[ch * 8u + q] = mb;
+    if (dl) {
 #pragma unroll
-    for (int j = 0; j < RTN_PD_S; ++j) a.counts[r * RTN_PD_S + j] = cnt[j];
+      for (int j = 0; j < RTN_PD_S; ++j) a.counts[r[u] * RTN_PD_S + j] = cnt[j];
+    }
   }
 }

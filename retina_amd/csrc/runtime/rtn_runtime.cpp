@@ -196,6 +196,15 @@ struct KArgs {
   uint64_t* conn_dlv;
 };
 
+// RTN_PD_GPW of the kernel (pc_kernel.hip; an RTN_KERNEL_DEFINES experiment may override it)
+uint32_t pd_groups_per_wave() {
+  const std::string d = env_defines();
+  size_t at = d.find("#define RTN_PD_GPW ");
+  if (at == std::string::npos) return 1u;
+  uint32_t g = (uint32_t)strtoul(d.c_str() + at + 19, nullptr, 10);
+  return (g == 1u || g == 2u || g == 4u || g == 8u) ? g : 1u;
+}
+
 // must match struct rtn_pd_args in pc_kernel.hip
 struct PdArgs {
   const uint64_t* fwd_bm;
@@ -488,7 +497,8 @@ int32_t rtn_pd_run(rtn_pc_t* pc, const rtn_pc_out_t* out, const rtn_ct_entry_t* 
   a.pd_bm = pd_bitmap;
   void* params[] = {&a};
   const uint32_t chunks = (n + RTN_CHUNK_FRAMES - 1u) / RTN_CHUNK_FRAMES;
-  hipError_t e = hipModuleLaunchKernel(pc->fn_pd, chunks, 1, 1, RTN_CHUNK_FRAMES, 1, 1, 0, s, params, nullptr);
+  const uint32_t threads = RTN_CHUNK_FRAMES / pd_groups_per_wave();  // RTN_PD_THREADS in pc_kernel.hip
+  hipError_t e = hipModuleLaunchKernel(pc->fn_pd, chunks, 1, 1, threads, 1, 1, 0, s, params, nullptr);
   if (e != hipSuccess) return fail(RTN_EDEVICE, std::string("hipModuleLaunchKernel: ") + hipGetErrorString(e));
   return RTN_OK;
 }
