@@ -373,6 +373,13 @@ __device__ __forceinline__ void rtn_flush(const rtn_args& a, const rtn_u64* ring
 #if defined(RTN_EXP_REC_STRIDE)
   // experiment: record regions RTN_EXP_REC_STRIDE records apart (overlapping: timing only)
   rtn_v4u* dst = reinterpret_cast<rtn_v4u*>(a.recs + ch.rec_base / (64u * RTN_CHUNK_GROUPS) * RTN_EXP_REC_STRIDE + ch.nflushed);
+#elif defined(RTN_EXP_REC_DENSE)
+  // experiment: records globally dense in flush order (one reservation per block; timing only)
+  rtn_u32 base = 0u;
+  if (lane == 0u) base = atomicAdd(&a.counters[3], (nrecs + 15u) & ~15u);
+  base = __shfl(base, 0);
+  const rtn_u64 cap = (rtn_u64)((a.n + 511u) / 512u) * 512u - 1024u;
+  rtn_v4u* dst = reinterpret_cast<rtn_v4u*>(a.recs + (((rtn_u64)base % cap) & ~15ull));
 #elif defined(RTN_EXP_REC_WRAP)
   // experiment: every chunk's records land in one of RTN_EXP_REC_WRAP regions (L2-resident)
   rtn_v4u* dst = reinterpret_cast<rtn_v4u*>(a.recs + (ch.rec_base / (64u * RTN_CHUNK_GROUPS) % RTN_EXP_REC_WRAP) * (64u * RTN_CHUNK_GROUPS) + ch.nflushed);
