@@ -271,6 +271,8 @@ class TableModel:
 #                                            T::from_mbuf(mbuf)`; datatypes/src/packet.rs:18-29
 #                                            Payload needs offset < data_len, offset+len <= data_len
 #
+# The tree is the oracle's own (filterlang.DeliverTree, restating filter_subtree + collapse for
+# FilterLayer::PacketDeliver); tests/test_pd.py also checks it against the compiler's export.
 # The connection-dependent conditions are given per connection as `facts` (fact index by the
 # predicate's text, as exported in Program.pd_program()["facts"]): a service fact is 1 when the
 # connection's service is that protocol; a session fact is the number of tracked sessions that

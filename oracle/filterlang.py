@@ -1142,3 +1142,222 @@ class PacketTree:
 
         rec(self.root, "", True)
         return "Tree Pkt (pass)\n," + "\n".join(lines) + "\n"
+
+
+# ----------------------------------------------------------------------------------------------
+# PacketDeliver tree (FilterLayer::PacketDeliver): filter_subtree + collapse for the packet
+# deliver filter. Only packet-level subscriptions take part (ptree.rs:330-333); no layer stops
+# a pattern and no actions are attached (with_term_filter / with_nonterm_filter are empty there,
+# datatypes.rs:704-721), so a node carries its predicate and its deliveries only.
+
+def _node_label(n: Node) -> str:
+    s = str(n.pred)
+    if n.deliver:
+        s += " D: ( " + "".join(n.deliver[k][0] + ", " for k in sorted(n.deliver)) + ")"
+    if n.if_else:
+        s += " x"
+    return s
+
+
+def _paths_lbl(n: Node) -> list[str]:
+    out = []
+
+    def rec(node, acc):
+        if not node.kids and acc:
+            out.append(",".join(acc))
+            return
+        for k in node.kids:
+            rec(k, acc + [_node_label(k)])
+
+    rec(n, [])
+    return out
+
+
+def _all_paths_eq(a: Node, b: Node) -> bool:
+    if not a.kids and not b.kids:
+        return True
+    return _paths_lbl(a) == _paths_lbl(b)
+
+
+def _windows_all_excl(kids: list) -> bool:
+    return all(is_excl(kids[k - 1].pred, kids[k].pred) for k in range(1, len(kids)))
+
+
+class DeliverTree:
+    """PTree for FilterLayer::PacketDeliver built by filter_subtree + collapse (ptree.rs)."""
+
+    def __init__(self, subs: list[Sub]):
+        self.subs = subs
+        self.root = Node(Pred("ethernet"))
+        self.size = 1
+        for sid, sub in enumerate(subs):
+            validate(sub)
+            if sub.level != "Packet":       # add_filter (ptree.rs:330-333)
+                continue
+            self._build(sid, sub, filter_patterns(sub.filter))
+        self._collapse()
+
+    # build_tree (ptree.rs:344-385): a pattern whose predicates all resolve at an earlier layer
+    # (for a packet-level subscription: all on_packet, ast.rs pred_is_prev_layer) is skipped --
+    # it was delivered at PacketContinue; nothing is attached to the root for PacketDeliver
+    def _build(self, sid, sub, patterns):
+        deliver = (sub.as_str, "FilterStr" in sub.datatypes)
+        for pat in patterns:
+            if all(on_packet(p) for p in pat):
+                continue
+            self._add_pattern(sid, deliver, pat)
+
+    # add_pattern (ptree.rs:389-461)
+    def _add_pattern(self, sid, deliver, pat):
+        node = self.root
+        for p in pat:
+            if req_packet(p):
+                raise FilterError("Cannot access per-packet fields (e.g., TCP flags, length) after packet filter.")
+            d = PacketTree._descendant(node, p)
+            if d is not None:
+                node = d
+                continue
+            par = PacketTree._narrowest_parent(node, p)
+            if par is not None:
+                node = par
+            moved = [k for k in node.kids if is_child(k.pred, p)]
+            node.kids = [k for k in node.kids if not is_child(k.pred, p)]
+            nxt = next((k for k in node.kids if k.pred == p), None)
+            if nxt is None:
+                nxt = Node(p, id=self.size)
+                self.size += 1
+                node.kids.append(nxt)
+            nxt.kids += moved
+            node = nxt
+        node.deliver[sid] = deliver          # should_deliver(PacketDeliver) for packet-level data
+
+    @staticmethod
+    def _extracts_protocol(n: Node) -> bool:
+        """ptree.rs:206-222 at PacketDeliver."""
+        if n.pred.unary and any(k.pred.unary for k in n.kids):
+            return True
+        if not n.pred.unary:
+            return False
+        return any(k.pred.proto == n.pred.proto and not k.pred.unary for k in n.kids)
+
+    def _collapse(self):
+        # ptree.rs:752-767: one possible callback needs no condition
+        seen: dict = {}
+
+        def single(n):
+            for k, v in n.deliver.items():
+                seen[k] = v
+            if len(seen) > 1:
+                return
+            for c in n.kids:
+                single(c)
+
+        single(self.root)
+        if len(seen) == 1:
+            self.root = Node(Pred("ethernet"), deliver=dict(seen))
+            self.size = 1
+            return
+
+        # prune_redundant_branches (ptree.rs:693-748); every predicate is a previous layer's here
+        def redundant(n, can_prune):
+            nxt = _windows_all_excl(n.kids)
+            for c in n.kids:
+                redundant(c, nxt)
+            if not can_prune:
+                return
+            must, could = [], []
+            for c in n.kids:
+                (must if c.deliver or self._extracts_protocol(c) else could).append(c)
+            nc = []
+            for c in could:
+                if all(_all_paths_eq(c, o) for o in n.kids):
+                    nc += c.kids
+                else:
+                    nc.append(c)
+            nc += must
+            nc = _stable_sort(nc)
+            dd = []
+            for c in nc:
+                if not dd or not (dd[-1].pred == c.pred and dd[-1].deliver == c.deliver):
+                    dd.append(c)
+            n.kids = dd
+
+        redundant(self.root, _windows_all_excl(self.root.kids))
+
+        # prune_packet_conditions (ptree.rs:641-687)
+        def packet_conds(n, can_prune):
+            if not on_packet(n.pred):
+                return
+            nxt = _windows_all_excl(n.kids)
+            for c in n.kids:
+                packet_conds(c, nxt)
+            if not can_prune:
+                return
+            while len(n.kids) == 1 and on_packet(n.kids[0].pred):
+                c = n.kids[0]
+                if self._extracts_protocol(c):
+                    break
+                n.deliver.update(c.deliver)
+                n.kids = c.kids
+
+        packet_conds(self.root, _windows_all_excl(self.root.kids))
+
+        # prune_branches (ptree.rs:570-634), deliveries only
+        def prune(n, on_d):
+            my_d = set(on_d)
+            keep = {}
+            for k in sorted(n.deliver):
+                s, must = n.deliver[k]
+                if s not in my_d:
+                    my_d.add(s)
+                    keep[k] = n.deliver[k]
+                elif must:
+                    keep[k] = n.deliver[k]
+            n.deliver = keep
+            for c in n.kids:
+                prune(c, my_d)
+            n.kids = [c for c in n.kids if c.kids or c.deliver]
+
+        prune(self.root, set())
+
+        def srt(n):
+            for c in n.kids:
+                srt(c)
+            n.kids = _stable_sort(n.kids)
+
+        srt(self.root)
+
+        def mark(n):
+            for i, c in enumerate(n.kids):
+                mark(c)
+                if i == 0:
+                    continue
+                prev = n.kids[i - 1]
+                if is_excl(c.pred, prev.pred):
+                    c.if_else = True
+                if c.deliver == prev.deliver and _all_paths_eq(c, prev):
+                    c.if_else = True
+
+        mark(self.root)
+        counter = [0]
+
+        def number(n):
+            n.id = counter[0]
+            counter[0] += 1
+            for c in n.kids:
+                number(c)
+
+        number(self.root)
+        self.size = counter[0]
+
+    def structure(self, n: Node | None = None):
+        """(predicate text, delivered subscription ids, if_else, children) for comparisons."""
+        n = self.root if n is None else n
+        return (str(n.pred), sorted(n.deliver), n.if_else, [self.structure(c) for c in n.kids])
+
+    def to_json(self, n: Node | None = None) -> dict:
+        """The tree in the shape of the compiler's JSON export (Program.tree_json)."""
+        n = self.root if n is None else n
+        return {"id": n.id, "pred": str(n.pred), "unary": n.pred.unary, "protocol": n.pred.proto, "data": 0,
+                "terminal": 0, "if_else": n.if_else, "deliver": sorted(n.deliver), "stream": [],
+                "children": [self.to_json(c) for c in n.kids]}

@@ -1,11 +1,12 @@
 """PacketDeliver filter (include/retina_pd.h): the generated `packet_deliver` for the frames of
 connections that hold the PacketDeliver action.
 
-CPU tests pin the compiler's statement table and fact list against the oracle's own numbering of
-the collapsed tree (oracle/conn.py DeliverFilter), the single-callback collapse
-(ptree.rs:752-767), the session-loop replay, and hand-checked outcomes. The GPU test runs two
+CPU tests pin the compiler's collapsed PacketDeliver tree against the oracle's own restatement
+(oracle/filterlang.py DeliverTree) on fixed and random subscription sets, the statement table and
+fact list against the oracle's numbering (oracle/conn.py DeliverFilter), the single-callback
+collapse (ptree.rs:752-767), the session-loop replay, and hand-checked outcomes. The GPU test runs
 batches through rtn_pc_run -> rtn_ct_process -> rtn_pd_run with random per-connection state and
-compares every frame's callback sequence with the oracle's, exactly."""
+compares every frame's callback sequence with the oracle's (on the oracle's own tree), exactly."""
 from __future__ import annotations
 
 import numpy as np
@@ -13,6 +14,7 @@ import pytest
 
 import helpers
 from oracle import conn as oconn
+from oracle import filterlang
 from retina_amd import pc
 
 SPEC = """
@@ -54,10 +56,53 @@ callback = "conn_cb"
 
 
 def _setup(spec: str = SPEC):
+    """Product program, its packet_deliver description, and the oracle's evaluator on the oracle's
+    own tree (the facts are named by predicate text, which is the host interface)."""
     prog = pc.Program.from_spec(spec)
     pd = prog.pd_program()
-    df = oconn.DeliverFilter(prog.tree_json(2), helpers.subs_from_spec(spec), [f["pred"] for f in pd["facts"]])
+    subs = helpers.subs_from_spec(spec)
+    tree = filterlang.DeliverTree(subs).to_json()
+    df = oconn.DeliverFilter(tree, subs, [f["pred"] for f in pd["facts"]])
     return prog, pd, df
+
+
+def _shape(j: dict):
+    return (j["pred"], sorted(j["deliver"]), j["if_else"], [_shape(c) for c in j["children"]])
+
+
+PD_FILTERS = ["tls", "http", "dns", "quic", "ssh", "tcp.port = 80 and http", "ipv4.addr = 10.0.0.0/8 and tls",
+              "tls.sni ~ 'a'", "http.user_agent ~ 'curl' and tcp.dst_port = 8080", "ipv6 and dns",
+              "udp.port = 53 and dns", "tcp.port >= 1000 and ssh", "tls.sni = 'x.com'",
+              "http.method = 'GET' and http.user_agent ~ 'a'", "ipv4.src_addr = 1.2.3.0/24 and quic",
+              "tcp.port = 443", "udp", "ipv6.dst_addr = 2001:db8::/32 and tls.sni ~ 'b'", "tls or http",
+              "tcp.dst_port = 443 and tls"]
+
+
+def _random_spec(rng) -> str:
+    out = []
+    for k in range(int(rng.integers(2, 7))):
+        f = PD_FILTERS[int(rng.integers(0, len(PD_FILTERS)))]
+        r = rng.random()
+        dts = ['"ZcFrame"'] if r < 0.4 else ['"Payload"'] if r < 0.6 else ['"ZcFrame"', '"FilterStr"'] if r < 0.8 \
+            else ['"ConnRecord"']
+        out.append(f'[[subscriptions]]\nfilter = "{f}"\ndatatypes = [{", ".join(dts)}]\ncallback = "cb{k}"\n')
+    return "\n".join(out)
+
+
+def test_pd_tree_matches_oracle_restatement():
+    for spec in [SPEC]:
+        prog = pc.Program.from_spec(spec)
+        assert _shape(prog.tree_json(2)) == _shape(filterlang.DeliverTree(helpers.subs_from_spec(spec)).to_json())
+    rng = np.random.default_rng(4)
+    nontrivial = 0
+    for _ in range(80):
+        spec = _random_spec(rng)
+        prog = pc.Program.from_spec(spec)
+        want = filterlang.DeliverTree(helpers.subs_from_spec(spec))
+        assert _shape(prog.tree_json(2)) == _shape(want.to_json()), spec
+        assert prog.info["pd_tree_size"] == want.size
+        nontrivial += want.size > 1
+    assert nontrivial > 25
 
 
 def test_pd_statement_table_matches_oracle_numbering():
