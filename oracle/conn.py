@@ -12,12 +12,13 @@
   filtergen/src/utils.rs:251-285           update_body: actions, then delivers, then streams
   include/retina_pc.h (rtn_conn_t)         the hash this repo defines over the canonical ConnId
 
-The FilterLayer::Packet tree itself is taken from the product compiler's JSON export
-(Program.tree_json(1)): the tree build is pinned by the reference's own ptree.rs KATs
-(tests/cpp/test_kats.cpp: core_ptree_packet, core_ptree_with_children, multi_ptree,
-core_ptree_prune), and what this module restates independently is its evaluation on the frame's
-bytes -- re-parsing the headers as packet_filter's parse_to chain does -- where the kernel
-evaluates it on the L4Context view it already holds.
+The FilterLayer::Packet tree is the oracle's own (filterlang.ConnTree: filter_subtree + collapse
+with SubscriptionSpec::packet_filter's actions, restated from ptree.rs / datatypes.rs); the
+compiler's tree is checked against it on every filter set and on random subscription sets
+(tests/test_conn.py), and the compiler's tree build is also pinned by the reference's own
+ptree.rs KATs (tests/cpp/test_kats.cpp). This module evaluates that tree on the frame's bytes --
+re-parsing the headers as packet_filter's parse_to chain does -- where the kernel evaluates it
+on the L4Context view it already holds.
 """
 from __future__ import annotations
 

@@ -1361,3 +1361,341 @@ class DeliverTree:
         return {"id": n.id, "pred": str(n.pred), "unary": n.pred.unary, "protocol": n.pred.proto, "data": 0,
                 "terminal": 0, "if_else": n.if_else, "deliver": sorted(n.deliver), "stream": [],
                 "children": [self.to_json(c) for c in n.kids]}
+
+
+# ----------------------------------------------------------------------------------------------
+# Packet-layer tree (FilterLayer::Packet): the first-packet `packet_filter` tree. Subscriptions
+# attach the actions of SubscriptionSpec::packet_filter (datatypes.rs:306-345, 626-637) and
+# deliver static-only data on the first packet (datatypes.rs:226-236).
+
+ACT = {"PacketContinue": 1 << 0, "PacketDeliver": 1 << 1, "PacketCache": 1 << 2, "PacketTrack": 1 << 3,
+       "ProtoProbe": 1 << 4, "ProtoFilter": 1 << 5, "SessionFilter": 1 << 6, "SessionDeliver": 1 << 7,
+       "SessionTrack": 1 << 8, "UpdatePDU": 1 << 9, "Reassemble": 1 << 10, "ConnDeliver": 1 << 11,
+       "Stream": 1 << 12}   # actions.rs:17-49 (bit order pinned by test_actions, actions.rs:390-421)
+
+# typedefs.rs:15-86 with the DataType constructors of datatypes.rs:108-198:
+# name -> (level, needs_parse, needs_update, needs_reassembly, needs_packet_track)
+_DT = {}
+for _n in ("ConnRecord", "ConnDuration", "PktCount", "ByteCount", "InterArrivals", "ConnHistory"):
+    _DT[_n] = ("Connection", False, True, False, False)
+for _n in ("HttpTransaction", "DnsTransaction", "TlsHandshake", "QuicStream", "SshHandshake"):
+    _DT[_n] = ("Session", True, False, False, False)
+for _n in ("ZcFrame", "Payload"):
+    _DT[_n] = ("Packet", False, False, False, False)
+_DT["SessionList"] = ("Connection", True, False, False, False)
+for _n in ("BidirZcPktStream", "OrigZcPktStream", "RespZcPktStream", "BidirPktStream", "OrigPktStream", "RespPktStream"):
+    _DT[_n] = ("Connection", False, False, False, True)
+for _n in ("OrigZcPktsReassembled", "RespZcPktsReassembled", "OrigPktsReassembled", "RespPktsReassembled"):
+    _DT[_n] = ("Connection", False, False, True, True)
+for _n in ("CoreId", "FiveTuple", "EtherTCI", "EthAddr", "FilterStr"):
+    _DT[_n] = ("Static", False, False, False, False)
+
+
+def _dt_packet_filter(name: str, sub_level: str) -> tuple[list[int], list[int]]:
+    """DataType::packet_filter (datatypes.rs:306-345): ([data, terminal] if matched, if matching)."""
+    lvl, parse, upd, reas, track = _DT[name]
+    m, g = [0, 0], [0, 0]
+    if lvl == "Packet" and sub_level == "Packet":
+        g[0] |= ACT["PacketCache"]
+    for flag, bit in ((upd, "UpdatePDU"), (reas, "Reassemble"), (track, "PacketTrack")):   # needs_update
+        if flag:
+            m[0] |= ACT[bit]
+            m[1] |= ACT[bit]
+            g[0] |= ACT[bit]
+    if sub_level == "Connection":                                                          # conn_deliver
+        m[0] |= ACT["ConnDeliver"]
+        m[1] |= ACT["ConnDeliver"]
+    if parse:
+        m[0] |= ACT["ProtoProbe"]
+        m[1] |= ACT["ProtoProbe"]
+        if sub_level == "Connection":
+            m[0] |= ACT["SessionTrack"]
+            m[1] |= ACT["SessionTrack"]
+    if lvl == "Session" and sub_level in ("Session", "Streaming"):
+        m[0] |= ACT["SessionDeliver"]
+        m[1] |= ACT["SessionDeliver"]
+    return m, g
+
+
+def _sub_packet_filter(sub: Sub) -> tuple[tuple[int, int], tuple[int, int]]:
+    """SubscriptionSpec::packet_filter (datatypes.rs:626-637)."""
+    m, g = [0, 0], [0, 0]
+    for d in sub.datatypes:
+        a, b = _dt_packet_filter(d, sub.level)
+        m = [m[0] | a[0], m[1] | a[1]]
+        g = [g[0] | b[0], g[1] | b[1]]
+    g[0] |= ACT["ProtoFilter"]
+    if sub.level == "Streaming":
+        m[0] |= ACT["Stream"]
+        m[1] |= ACT["Stream"]
+    return (m[0], m[1]), (g[0], g[1])
+
+
+def _can_stream(level: str) -> bool:
+    return level in ("Connection", "Packet")
+
+
+def _pkt_should_deliver(sub: Sub, p: Pred) -> bool:
+    """SubscriptionSpec::should_deliver at FilterLayer::Packet (datatypes.rs:563-573, 203-265):
+    only static data of a static-only subscription is delivered there, on a packet predicate."""
+    if sub.level == "Streaming":
+        return False
+    lv = [_DT[d][0] for d in sub.datatypes]
+    anyd = any(l == "Static" and sub.level == "Static" and on_packet(p) for l in lv)
+    alld = all(l in ("Packet", "Static") for l in lv)                        # can_deliver
+    return anyd and alld
+
+
+def _pkt_should_stream(sub: Sub, p: Pred) -> bool:
+    """SubscriptionSpec::should_stream at FilterLayer::Packet (datatypes.rs:584-615)."""
+    if sub.level != "Streaming":
+        return False
+    lv = [_DT[d][0] for d in sub.datatypes]
+    if any(l not in ("Packet", "Static") and not _can_stream(l) for l in lv):
+        return False
+    if all(_can_stream(l) or l == "Static" for l in lv):
+        return on_packet(p)
+    return False   # no datatype's should_deliver holds at the Packet layer for a streaming sub
+
+
+@dataclass
+class CNode:
+    pred: Pred
+    id: int = 0
+    data: int = 0
+    term: int = 0
+    deliver: dict = field(default_factory=dict)   # sid -> (as_str, must_deliver)
+    stream: dict = field(default_factory=dict)
+    kids: list = field(default_factory=list)
+    if_else: bool = False
+
+    def label(self) -> str:
+        s = str(self.pred)
+        if self.data or self.term:
+            s += f" -- A: {self.data}/{self.term}"
+        if self.deliver:
+            s += " D: ( " + "".join(self.deliver[k][0] + ", " for k in sorted(self.deliver)) + ")"
+        if self.stream:
+            s += " S: ( " + "".join(self.stream[k][0] + ", " for k in sorted(self.stream)) + ")"
+        if self.if_else:
+            s += " x"
+        return s
+
+    def same(self, o: "CNode") -> bool:          # PartialEq for PNode (ptree.rs:871-876)
+        return self.pred == o.pred and (self.data, self.term) == (o.data, o.term) and self.deliver == o.deliver
+
+
+def _cpaths(n: CNode) -> list[str]:
+    out = []
+
+    def rec(node, acc):
+        if not node.kids and acc:
+            out.append(",".join(acc))
+            return
+        for k in node.kids:
+            rec(k, acc + [k.label()])
+
+    rec(n, [])
+    return out
+
+
+def _c_all_paths_eq(a: CNode, b: CNode) -> bool:
+    return (not a.kids and not b.kids) or _cpaths(a) == _cpaths(b)
+
+
+class ConnTree:
+    """PTree for FilterLayer::Packet built by filter_subtree + collapse (ptree.rs)."""
+
+    def __init__(self, subs: list[Sub]):
+        self.subs = subs
+        self.root = CNode(Pred("ethernet"))
+        self.size = 1
+        for sid, sub in enumerate(subs):
+            validate(sub)
+            self._build(sid, sub, filter_patterns(sub.filter))
+        self._collapse()
+
+    # build_tree (ptree.rs:344-385)
+    def _build(self, sid, sub, patterns):
+        deliver = (sub.as_str, "FilterStr" in sub.datatypes)
+        prev = lambda p: on_packet(p) and sub.level == "Packet"  # noqa: E731  is_prev_layer (ast.rs:173-176)
+        added = False
+        for pat in patterns:
+            if all(prev(p) for p in pat):
+                continue
+            added = added or bool(pat)
+            self._add_pattern(sid, sub, deliver, pat)
+        eth = Pred("ethernet")
+        if not added and prev(eth) and not _pkt_should_stream(sub, eth):
+            return
+        if not added:
+            if _pkt_should_deliver(sub, eth):
+                self.root.deliver[sid] = deliver
+            elif _pkt_should_stream(sub, eth):
+                self.root.stream[sid] = deliver
+            else:
+                (m, _) = _sub_packet_filter(sub)
+                self.root.data |= m[0]
+                self.root.term |= m[1]
+
+    # add_pattern (ptree.rs:389-461)
+    def _add_pattern(self, sid, sub, deliver, pat):
+        node = self.root
+        matched, matching = _sub_packet_filter(sub)
+        for p in pat:
+            if not on_packet(p):                 # is_next_layer: non-terminal leaf
+                node.data |= matching[0]
+                node.term |= matching[1]
+                return
+            if req_packet(p):
+                raise FilterError("Cannot access per-packet fields (e.g., TCP flags, length) after packet filter.")
+            d = PacketTree._descendant(node, p)
+            if d is not None:
+                node = d
+                continue
+            par = PacketTree._narrowest_parent(node, p)
+            if par is not None:
+                node = par
+            moved = [k for k in node.kids if is_child(k.pred, p)]
+            node.kids = [k for k in node.kids if not is_child(k.pred, p)]
+            nxt = next((k for k in node.kids if k.pred == p), None)
+            if nxt is None:
+                nxt = CNode(p, id=self.size)
+                self.size += 1
+                node.kids.append(nxt)
+            nxt.kids += moved
+            node = nxt
+        if _pkt_should_deliver(sub, node.pred):
+            node.deliver[sid] = deliver
+        elif _pkt_should_stream(sub, node.pred):
+            node.stream[sid] = deliver
+        node.data |= matched[0]
+        node.term |= matched[1]
+
+    @staticmethod
+    def _extracts_protocol(n: CNode) -> bool:
+        if n.pred.unary and any(k.pred.unary for k in n.kids):
+            return True
+        if not n.pred.unary:
+            return False
+        return any(k.pred.proto == n.pred.proto and not k.pred.unary for k in n.kids)
+
+    def _collapse(self):
+        ex = _windows_all_excl
+
+        def redundant(n, can_prune):                 # ptree.rs:693-748
+            if not on_packet(n.pred):
+                return
+            nxt = ex(n.kids)
+            for c in n.kids:
+                redundant(c, nxt)
+            if not can_prune:
+                return
+            must, could = [], []
+            for c in n.kids:
+                keep = c.data or c.term or c.stream or c.deliver or not on_packet(c.pred) or self._extracts_protocol(c)
+                (must if keep else could).append(c)
+            nc = []
+            for c in could:
+                if all(_c_all_paths_eq(c, o) for o in n.kids):
+                    nc += c.kids
+                else:
+                    nc.append(c)
+            nc = _stable_sort(nc + must)
+            dd = []
+            for c in nc:
+                if not dd or not dd[-1].same(c):
+                    dd.append(c)
+            n.kids = dd
+
+        redundant(self.root, ex(self.root.kids))
+
+        def packet_conds(n, can_prune):              # ptree.rs:641-687
+            if not on_packet(n.pred):
+                return
+            nxt = ex(n.kids)
+            for c in n.kids:
+                packet_conds(c, nxt)
+            if not can_prune:
+                return
+            while len(n.kids) == 1 and on_packet(n.kids[0].pred):
+                c = n.kids[0]
+                if self._extracts_protocol(c):
+                    break
+                n.data |= c.data
+                n.term |= c.term
+                n.deliver.update(c.deliver)
+                n.stream.update(c.stream)
+                n.kids = c.kids
+
+        packet_conds(self.root, ex(self.root.kids))
+
+        def prune(n, on_a, on_d, on_s):              # ptree.rs:570-634
+            my_d = set(on_d)
+            keep = {}
+            for k in sorted(n.deliver):
+                s, must = n.deliver[k]
+                if s not in my_d:
+                    my_d.add(s)
+                    keep[k] = n.deliver[k]
+                elif must:
+                    keep[k] = n.deliver[k]
+            n.deliver = keep
+            my_s = set(on_s)
+            keep = {}
+            for k in sorted(n.stream):
+                s, must = n.stream[k]
+                if s not in my_s:
+                    my_s.add(s)
+                    keep[k] = n.stream[k]
+                elif must:
+                    keep[k] = n.stream[k]
+            n.stream = keep
+            my_a = on_a
+            if n.data or n.term:
+                n.data &= ~on_a                      # Actions::clear_intersection (actions.rs)
+                n.term &= ~on_a
+                my_a = on_a | n.data
+                # push: data and terminal both accumulate; clear_intersection only reads `data`
+            for c in n.kids:
+                prune(c, my_a, my_d, my_s)
+            n.kids = [c for c in n.kids if c.data or c.term or c.kids or c.deliver]
+
+        prune(self.root, 0, set(), set())
+
+        def srt(n):
+            for c in n.kids:
+                srt(c)
+            n.kids = _stable_sort(n.kids)
+
+        srt(self.root)
+
+        def mark(n):                                 # ptree.rs:527-552
+            for i, c in enumerate(n.kids):
+                mark(c)
+                if i == 0:
+                    continue
+                prev = n.kids[i - 1]
+                if is_excl(c.pred, prev.pred):
+                    c.if_else = True
+                if (c.data, c.term) == (prev.data, prev.term) and c.deliver == prev.deliver and \
+                        _c_all_paths_eq(c, prev):
+                    c.if_else = True
+
+        mark(self.root)
+        counter = [0]
+
+        def number(n):
+            n.id = counter[0]
+            counter[0] += 1
+            for c in n.kids:
+                number(c)
+
+        number(self.root)
+        self.size = counter[0]
+
+    def to_json(self, n: CNode | None = None) -> dict:
+        n = self.root if n is None else n
+        return {"id": n.id, "pred": str(n.pred), "unary": n.pred.unary, "protocol": n.pred.proto, "data": n.data,
+                "terminal": n.term, "if_else": n.if_else, "deliver": sorted(n.deliver), "stream": sorted(n.stream),
+                "children": [self.to_json(c) for c in n.kids]}

@@ -86,8 +86,8 @@ def python_crosscheck(spec: str, slab: np.ndarray, dlen: np.ndarray, res: dict, 
 
 def conn_expected(spec: str, slab: np.ndarray, dlen: np.ndarray, fwd: np.ndarray) -> tuple[np.ndarray, np.ndarray]:
     """Connection stage of the forwarded frames, in frame order: (hash, info) and statement masks."""
-    prog = rpc.Program.from_spec(spec)
-    pf = conn.PacketFilter(prog.tree_json(1), filterlang.load_spec(spec))
+    subs = filterlang.load_spec(spec)
+    pf = conn.PacketFilter(filterlang.ConnTree(subs).to_json(), subs)
     words = max(1, (len(pf.stmts) + 63) // 64)
     b = slab.reshape(-1, STRIDE)
     idx = np.nonzero(fwd)[0]

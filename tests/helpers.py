@@ -94,7 +94,8 @@ def oracle_conn(spec: str, slab: np.ndarray, stride: int, dlen: np.ndarray, fwd:
     from oracle import conn as oconn
     from retina_amd import pc
 
-    pf = oconn.PacketFilter(pc.Program.from_spec(spec).tree_json(1), subs_from_spec(spec))
+    subs = subs_from_spec(spec)
+    pf = oconn.PacketFilter(filterlang.ConnTree(subs).to_json(), subs)
     words = max(1, (len(pf.stmts) + 63) // 64)
     b = np.ascontiguousarray(slab, np.uint8).reshape(-1, stride)
     idx = np.nonzero(fwd)[0]

@@ -15,6 +15,7 @@ import pytest
 import helpers
 from golden.filter_sets import SETS
 from oracle import conn as oconn
+from oracle import filterlang
 from oracle import packet
 from retina_amd import pc, synth
 
@@ -89,10 +90,55 @@ def test_per_packet_fields_after_packet_filter_are_rejected(filt, dts):
 @pytest.mark.parametrize("fset", list(SETS))
 def test_statement_table_matches_oracle(fset):
     prog = pc.Program.from_spec(SETS[fset])
-    pf = oconn.PacketFilter(prog.tree_json(1), helpers.subs_from_spec(SETS[fset]))
+    subs = helpers.subs_from_spec(SETS[fset])
+    pf = oconn.PacketFilter(filterlang.ConnTree(subs).to_json(), subs)
     subs, kinds = prog.conn_table()
     assert [(int(s), int(k)) for s, k in zip(subs, kinds)] == pf.stmts
     assert prog.info["n_conn_stmts"] == len(pf.stmts)
+
+
+def _cshape(j: dict):
+    return (j["pred"], j["data"], j["terminal"], sorted(j["deliver"]), sorted(j["stream"]), j["if_else"],
+            [_cshape(c) for c in j["children"]])
+
+
+CONN_FILTERS = ["tcp.port = 80", "ipv4.addr = 10.0.0.0/8 and tcp", "tls", "http and tcp.port != 80", "udp.port = 53",
+                "ipv6.dst_addr = 2001:db8::/32 and udp", "tcp.src_port >= 1024 and ipv4.dst_addr != 10.0.0.0/8",
+                "dns and ((tcp and tcp.port != 53) or (udp and udp.port != 53))", "tls.sni ~ 'a'", "ipv4 or ipv6",
+                "quic", "ssh and tcp.dst_port = 22", "tcp.dst_port in 1000..2000", "", "udp"]
+CONN_DTS = [["ConnRecord"], ["FiveTuple"], ["FiveTuple", "FilterStr"], ["TlsHandshake"], ["ZcFrame"],
+            ["Payload", "CoreId"], ["PktCount", "FiveTuple"], ["SessionList"], ["OrigZcPktStream"],
+            ["HttpTransaction", "FiveTuple"], ["ConnRecord", "CoreId"]]
+
+
+def test_conn_tree_matches_oracle_restatement():
+    """The compiler's FilterLayer::Packet tree equals the oracle's (filterlang.ConnTree, a
+    restatement of filter_subtree + collapse with SubscriptionSpec::packet_filter's actions) on
+    every filter set and on random subscription sets."""
+    for fset, spec in SETS.items():
+        prog = pc.Program.from_spec(spec)
+        assert _cshape(prog.tree_json(1)) == _cshape(filterlang.ConnTree(helpers.subs_from_spec(spec)).to_json()), fset
+    rng = np.random.default_rng(8)
+    checked = 0
+    for _ in range(150):
+        subs = []
+        for k in range(int(rng.integers(1, 6))):
+            f = CONN_FILTERS[int(rng.integers(0, len(CONN_FILTERS)))]
+            d = CONN_DTS[int(rng.integers(0, len(CONN_DTS)))]
+            stream = ("packets=1",) if rng.random() < 0.1 and d in (["PktCount", "FiveTuple"], ["ConnRecord"]) else ()
+            subs.append((f, d, f"cb{k}", *stream))
+        spec = synth._toml(subs)
+        try:
+            prog = pc.Program.from_spec(spec)
+        except pc.FilterError:
+            with pytest.raises(filterlang.FilterError):
+                filterlang.ConnTree(helpers.subs_from_spec(spec))
+            continue
+        want = filterlang.ConnTree(helpers.subs_from_spec(spec))
+        assert _cshape(prog.tree_json(1)) == _cshape(want.to_json()), spec
+        assert prog.info["conn_tree_size"] == want.size
+        checked += 1
+    assert checked > 100
 
 
 def test_conn_tree_json_matches_display():

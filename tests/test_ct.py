@@ -10,6 +10,7 @@ import pytest
 import helpers
 from golden.filter_sets import SETS
 from oracle import conn as oconn
+from oracle import filterlang
 from oracle import packet
 from retina_amd import pc
 
@@ -49,7 +50,8 @@ class _Run:
         self.prog = pc.Program.from_spec(SPEC)
         self.ctx = pc.PacketContinue(self.prog, 0)
         self.ct = pc.ConnTable(0, cap_log2, max_conn)
-        self.pf = oconn.PacketFilter(self.prog.tree_json(1), helpers.subs_from_spec(SPEC))
+        subs = helpers.subs_from_spec(SPEC)
+        self.pf = oconn.PacketFilter(filterlang.ConnTree(subs).to_json(), subs)
 
     def batch(self, frames):
         torch = self.torch

@@ -16,6 +16,7 @@ import pytest
 import helpers
 from golden.filter_sets import SETS
 from oracle import conn as oconn
+from oracle import filterlang
 from oracle import packet
 from retina_amd import pc
 
@@ -66,7 +67,8 @@ def test_offline_runtime_vs_oracle(gpu, tmp_path):
     assert summary["forwarded"] == len(idx) and summary["packet_continue"] == int(ora["pc"].sum())
 
     prog = pc.Program.from_spec(SPEC)
-    pf = oconn.PacketFilter(prog.tree_json(1), helpers.subs_from_spec(SPEC))
+    subs = helpers.subs_from_spec(SPEC)
+    pf = oconn.PacketFilter(filterlang.ConnTree(subs).to_json(), subs)
     model = oconn.TableModel()
     exp_status = []
     for b0 in range(0, len(kept), batch):
