@@ -207,16 +207,25 @@ int main(int argc, char** argv) {
 
   Totals t;
   uint64_t next_frame = 0;
+  double t_wait = 0, t_walk = 0, t_pack = 0;  // host time split (seconds)
+  auto now = [] { return std::chrono::steady_clock::now(); };
+  auto secs_since = [&](std::chrono::steady_clock::time_point a) { return std::chrono::duration<double>(now() - a).count(); };
   const auto t0 = std::chrono::steady_clock::now();
   for (uint32_t it = 0;; ++it) {
     HostSet& h = hs[it & 1u];
     if (h.pending) {  // results of batch it-2 (same buffers): wait, then walk them
+      auto a = now();
       HIP_CHECK(hipEventSynchronize(done[it & 1u]));
+      t_wait += secs_since(a);
+      a = now();
       walk(h, with_ct, t, dump);
+      t_walk += secs_since(a);
       h.pending = false;
     }
     uint32_t n = 0;
+    const auto tp = now();
     RTN_CHECK(rtn_pcap_next_batch(cap, h.slab, kStride, h.dlen, batch, &n));
+    t_pack += secs_since(tp);
     if (n == 0) break;
     h.n = n;
     h.first_frame = next_frame;
@@ -254,12 +263,14 @@ int main(int argc, char** argv) {
   printf("{\"frames_read\": %llu, \"skipped_mtu\": %llu, \"frames\": %llu, \"bytes\": %llu, \"packet_continue\": %llu, "
          "\"forwarded\": %llu, \"tcp\": %llu, \"udp\": %llu, \"ct\": {\"hit\": %llu, \"new\": %llu, \"miss\": %llu, "
          "\"new_dropped\": %llu, \"full\": %llu, \"collision\": %llu, \"prior\": %llu, \"live\": %u}, "
-         "\"seconds\": %.6f, \"mpps\": %.2f, \"batch\": %u}\n",
+         "\"seconds\": %.6f, \"mpps\": %.2f, \"batch\": %u, "
+         "\"host_s\": {\"pack\": %.4f, \"wait\": %.4f, \"walk\": %.4f}}\n",
          (unsigned long long)ps.frames, (unsigned long long)ps.skipped_mtu, (unsigned long long)t.frames,
          (unsigned long long)ps.bytes, (unsigned long long)t.pc, (unsigned long long)t.fwd, (unsigned long long)t.tcp,
          (unsigned long long)t.udp, (unsigned long long)t.status[1], (unsigned long long)t.status[2],
          (unsigned long long)t.status[3], (unsigned long long)t.status[4], (unsigned long long)t.status[5],
-         (unsigned long long)t.status[6], (unsigned long long)t.prior, cs.live, secs, t.frames / secs / 1e6, batch);
+         (unsigned long long)t.status[6], (unsigned long long)t.prior, cs.live, secs, t.frames / secs / 1e6, batch, t_pack, t_wait,
+         t_walk);
   if (dump) fclose(dump);
   rtn_pcap_close(cap);
   if (ct) rtn_ct_destroy(ct);

@@ -42,9 +42,28 @@ struct rtn_pcap {
   bool swap = false;    // file byte order differs from the host's
   uint32_t mtu = 0;
   rtn_pcap_stats_t st{};
+  size_t populated = 0;  // page tables mapped up to here (prefault)
 };
 
 namespace {
+
+// Map the page tables a batch will read in one call (MADV_POPULATE_READ, Linux 5.14+) instead of
+// taking a fault per 64 KB inside the packing loop. Best effort: older kernels fault as before.
+void prefault(rtn_pcap* p, size_t off, size_t bytes) {
+#ifdef MADV_POPULATE_READ
+  const size_t page = 4096, end = (p->size + page - 1) & ~(page - 1);
+  const size_t a = (off > p->populated ? off : p->populated) & ~(page - 1);
+  size_t b = (off + bytes + page - 1) & ~(page - 1);
+  if (b > end) b = end;
+  if (b <= a) return;
+  (void)madvise(const_cast<uint8_t*>(p->base) + a, b - a, MADV_POPULATE_READ);
+  p->populated = b;
+#else
+  (void)p;
+  (void)off;
+  (void)bytes;
+#endif
+}
 
 // Next frame of the capture: captured bytes + original length. Returns false at end of file
 // (a truncated trailing record ends the file, as libpcap does).
@@ -134,6 +153,8 @@ int32_t rtn_pcap_next_batch(rtn_pcap_t* p, uint8_t* slab, uint64_t stride, uint1
                             uint32_t* n) {
   if (!p || !slab || !data_len || !n) return rtn::set_error(RTN_EINVAL, "null argument");
   if (stride == 0) return rtn::set_error(RTN_EINVAL, "stride must be positive");
+  // about the bytes this batch reads: its frames at the capture's mean size so far, plus headers
+  prefault(p, p->off, (size_t)cap * (p->st.packed ? p->st.bytes / p->st.packed + 32u : 128u) + (1u << 20));
   uint32_t k = 0;
   while (k < cap) {
     const uint8_t* data;
