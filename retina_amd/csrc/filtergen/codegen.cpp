@@ -316,6 +316,54 @@ struct Gen {
     }
   }
 
+
+  // ---- PacketContinue as straight-line HIP (the default body): every node's reach flag is a
+  // select chain, actions and delivery bits are OR-ed in under their node's flag. A wave whose
+  // lanes take different branches runs all of them anyway; this form drops the exec-mask
+  // bookkeeping of each branch. Statement numbering follows children() / update_body().
+  uint32_t flat_pc_stmt = 0;
+  void pc_flat_body(const PNode& n, const std::string& R) {
+    if (!n.actions.drop()) hip += "  act |= " + R + " ? " + u32lit(n.actions.data) + " : 0u;\n";
+    for (auto& dv : n.deliver) {
+      uint32_t k = flat_pc_stmt++;
+      if (k >= prog.delivers.size() || prog.delivers[k].sub_id != (uint32_t)dv.id)
+        throw FilterError("internal: packet-continue statement order");
+      std::string reach = prog.delivers[k].payload ? "(" + R + " && v.payload_ok)" : R;
+      hip += "  dm[" + std::to_string(k / 64) + "] |= " + reach + " ? (1ull << " + std::to_string(k % 64) + ") : 0ull;\n";
+    }
+  }
+  void pc_flat(const PNode& n, const std::string& R) {
+    bool first_unary = true;
+    std::string T;
+    for (auto& c : n.children) {
+      if (!c.pred.on_packet()) continue;
+      const std::string id = std::to_string(c.id);
+      std::string cond;
+      bool is_else;
+      if (c.pred.is_unary()) {
+        const std::string& proto = c.pred.protocol;
+        cond = proto == "ipv4" ? "v.v4" : proto == "ipv6" ? "v.v6" : proto == "tcp" ? "v.tcp" : "v.udp";
+        is_else = !first_unary;
+        first_unary = false;
+      } else {
+        cond = binary(c.pred).first;
+        is_else = c.if_else;
+      }
+      const std::string rc = "r" + id;
+      hip += "  const bool k" + id + " = " + cond + ";\n";
+      if (!is_else || T.empty()) {
+        T = "t" + id;
+        hip += "  bool " + T + " = k" + id + ";\n";
+        hip += "  const bool " + rc + " = " + R + " && k" + id + ";\n";
+      } else {
+        hip += "  const bool " + rc + " = " + R + " && !" + T + " && k" + id + ";\n";
+        hip += "  " + T + " = " + T + " || k" + id + ";\n";
+      }
+      pc_flat(c, rc);
+      pc_flat_body(c, rc);
+    }
+  }
+
   // ---- FilterLayer::PacketDeliver (deliver_filter.rs) ----
   // The body multiplies `m` (how many times the enclosing session loops run it) into per-statement
   // counts; `f` holds the connection's facts (PdFact) and `pok` the Payload guard.
@@ -529,6 +577,16 @@ PacketProgram compile_packet_program(const std::vector<SubscriptionSpec>& subs) 
   if (prog.wraps_ethernet) {
     g.hip += "  }\n";
     g.rust += "  }\n";
+  }
+  prog.hip_body_branchy = "__device__ __forceinline__ void rtn_filter(const rtn_view& v, rtn_u32& act, rtn_u64* dm) {\n"
+                          "  (void)v; (void)dm;\n" +
+                          g.hip + "}\n";
+  g.hip.clear();
+  {
+    const std::string R0 = prog.wraps_ethernet ? "v.eth_ok" : "true";
+    if (root_body) g.pc_flat_body(root, R0);
+    g.pc_flat(root, R0);
+    if (g.flat_pc_stmt != prog.delivers.size()) throw FilterError("internal: packet-continue statement count");
   }
   prog.hip_body = "__device__ __forceinline__ void rtn_filter(const rtn_view& v, rtn_u32& act, rtn_u64* dm) {\n"
                   "  (void)v; (void)dm;\n" +
