@@ -264,3 +264,64 @@ def test_pd_gpu_vs_oracle(gpu):
         st_all = state.view(-1, 1 + nf)
         st_all[torch.from_numpy(live.astype(np.int64)).to(dev)] = torch.from_numpy(new.view(np.int32)).to(dev)
     assert checked > 1000 and delivered > 200
+
+
+@pytest.mark.gpu
+def test_pd_gpu_ragged_batches_and_no_packet_subscriptions(gpu):
+    import torch
+
+    from golden.filter_sets import SETS
+
+    prog, pd, df = _setup()
+    ctx = pc.PacketContinue(prog, 0)
+    ct = pc.ConnTable(0, 12)
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(12)
+    pool = _pd_pool(rng, 200)
+    nf = len(pd["facts"])
+    # open every flow, then give every connection PacketDeliver and facts of 1..2
+    opener = _pd_frames(rng, pool, 3000, 1.0)
+    slab, dlen = pc.pack_frames(opener, 128)
+    out = ctx.alloc_outputs(len(opener), conn=True)
+    ctx.run(torch.from_numpy(slab).to(dev), 128, torch.from_numpy(dlen.view(np.int16)).to(dev), len(opener), out)
+    ct.process(out)
+    st = np.zeros((ct.capacity, 1 + nf), np.uint32)
+    st[:, 0] = pc.PD_ACTIVE
+    st[:, 1:] = rng.integers(1, 3, (ct.capacity, nf))
+    state = torch.from_numpy(st.view(np.int32)).to(dev).reshape(-1)
+    for n in (1, 63, 65, 511, 513, 1025):
+        frames = _pd_frames(rng, pool, n, 0.0)
+        slab, dlen = pc.pack_frames(frames, 128)
+        d_dlen = torch.from_numpy(dlen.view(np.int16)).to(dev)
+        out = ctx.alloc_outputs(n, conn=True)
+        ctx.run(torch.from_numpy(slab).to(dev), 128, d_dlen, n, out)
+        ent = ct.process(out)
+        counts, bm = pc.pd_run(ctx, out, ent, d_dlen, state)
+        torch.cuda.synchronize()
+        bits = np.unpackbits(bm.cpu().numpy()[:((n + 63) // 64) * 8], bitorder="little")
+        assert not bits[n:].any(), n   # no bits past the batch
+        got_idx, got_cnt = pc.decode_pd(counts, bm, out, len(pd["stmts"]))
+        got = dict(zip(got_idx.tolist(), got_cnt))
+        fwd = np.nonzero(out.decode()["fwd"])[0]
+        e = pc.decode_ct(ent, out)
+        for j, i in enumerate(fwd):
+            slot, status = int(e[j, 0]), int(e[j, 1])
+            exp = []
+            if status == pc.CT_HIT | pc.CT_PRIOR:
+                exp = df.evaluate(frames[i], len(frames[i]), st[slot, 1:])
+            assert (i in got) == bool(exp), (n, i)
+            if exp:
+                assert pc.pd_replay(pd, got[i], st[slot, 1:]) == exp, (n, i)
+    # a program without packet-level subscriptions delivers nothing (the bitmap is cleared)
+    p2 = pc.PacketContinue(pc.Program.from_spec(SETS["cfg2"]), 0)
+    assert p2.program.info["n_pd_stmts"] == 0
+    out2 = p2.alloc_outputs(700, conn=True)
+    frames = _pd_frames(rng, pool, 700, 0.0)
+    slab, dlen = pc.pack_frames(frames, 128)
+    d_dlen = torch.from_numpy(dlen.view(np.int16)).to(dev)
+    p2.run(torch.from_numpy(slab).to(dev), 128, d_dlen, 700, out2)
+    ent2 = pc.ConnTable(0, 10).process(out2)
+    bm0 = torch.full((pc.lib().rtn_out_bitmap_bytes(700),), 0xFF, dtype=torch.uint8, device=dev)
+    _, bm2 = pc.pd_run(p2, out2, ent2, d_dlen, torch.zeros(1024, dtype=torch.int32, device=dev), bitmap=bm0)
+    torch.cuda.synchronize()
+    assert not bm2.cpu().numpy().any()
