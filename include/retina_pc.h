@@ -75,7 +75,8 @@ typedef struct rtn_l4ctx {
  *           then h ^= 16 (IPv4) or 40 (IPv6) and fmix32. max/min are Rust's SocketAddr order
  *           (ip, then port), as ConnId::new's cmp::max/min.
  *   info  = packet_filter Actions.data (13 bits) | terminal_actions << 13 | creates << 26 |
- *           src_is_max << 27 | any first-packet statement fired << 28. `creates`: the frame would
+ *           src_is_max << 27 | any first-packet statement fired << 28 | IPv6 << 29 | UDP << 30
+ *           (the last two repeat the record's, so later stages can skip the record). `creates`: the frame would
  *           open a connection on a table miss (TCP SYN without ACK/RST, or any UDP). The
  *           packet_filter result is that of this frame, which the host uses only when the frame
  *           does open a connection. */
@@ -88,6 +89,8 @@ typedef struct rtn_conn {
 #define RTN_CONN_CREATES(i) (((i) >> 26) & 1u)
 #define RTN_CONN_SRC_IS_MAX(i) (((i) >> 27) & 1u)
 #define RTN_CONN_PF_STMTS(i) (((i) >> 28) & 1u)
+#define RTN_CONN_IPV6(i) (((i) >> 29) & 1u) /* the record is IPv6 (its addresses are in addr6)  */
+#define RTN_CONN_UDP(i) (((i) >> 30) & 1u)  /* L4Context.proto is UDP (else TCP)              */
 
 /* A batch of frames laid out for coalesced HBM reads, in one of two layouts:
  *  - monolithic (ext == NULL): slot i (stride bytes, a multiple of 64) holds the first

@@ -43,7 +43,7 @@ extern "C" {
 
 #define RTN_PD_ACTIVE 1u /* state flags: the connection's actions hold PacketDeliver */
 
-/* Evaluate packet_deliver for the batch: `out` and `ct` as produced for the same n frames,
+/* Evaluate packet_deliver for the batch: `out` (with addr6 and conn) and `ct` as produced for the same n frames,
  * `data_len` the batch's (Payload needs the frame length), `state` [state_slots][1 + n_pd_facts]
  * in device memory. Writes pd_bitmap [ceil(n/64)] (frame has >= 1 delivery) and, for those
  * frames only, counts[record][n_pd_stmts] at the frame's record index (like l4 and ct). A

@@ -186,7 +186,7 @@ def stage(pf: PacketFilter, frame: bytes, dl: int) -> tuple[int, int, list[int]]
     h = conn_hash(ctx.ver == 6, mx[0], mn[0], mx[1], mn[1], ctx.proto)
     data, term, fired = pf.evaluate(frame, dl)
     info = (data & 0x1FFF) | ((term & 0x1FFF) << 13) | (int(creates(ctx)) << 26) | (int(gt) << 27) | \
-        (int(bool(fired)) << 28)
+        (int(bool(fired)) << 28) | (int(ctx.ver == 6) << 29) | (int(ctx.proto == 17) << 30)
     return h, info, fired
 
 

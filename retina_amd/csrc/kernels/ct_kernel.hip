@@ -172,12 +172,15 @@ __device__ __forceinline__ void rtn_ct_load(const rtn_ct_args& a, rtn_ct_frames&
   const rtn_u32 gj = c * (RTN_CT_CHUNK / 64u) + (lane & 7u);
   const rtn_u64 word = gj < nw ? a.fwd_bm[gj] : 0ull;
   const rtn_u32 pop = (rtn_u32)__popcll(word);
-  rtn_u32 pre[8];
-  rtn_u32 acc = 0u;
+  // (q = w * G + u is not a compile-time index: accumulate per group instead of indexing an array)
+  rtn_u32 pre[G];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    pre[j] = acc;
-    acc += __shfl(pop, j);
+  for (rtn_u32 u = 0; u < G; ++u) pre[u] = 0u;
+#pragma unroll
+  for (rtn_u32 j = 0; j < 8u; ++j) {
+    const rtn_u32 pj = __shfl(pop, (int)j);
+#pragma unroll
+    for (rtn_u32 u = 0; u < G; ++u) pre[u] += j < w * G + u ? pj : 0u;
   }
   rtn_u64 m6[G];
 #pragma unroll
@@ -185,26 +188,18 @@ __device__ __forceinline__ void rtn_ct_load(const rtn_ct_args& a, rtn_ct_frames&
     const rtn_u32 q = w * G + u;  // group within the chunk
     const rtn_u64 m = __shfl(word, (int)q);
     f.has[u] = c * (RTN_CT_CHUNK / 64u) + q < nw && ((m >> lane) & 1ull);
-    f.r[u] = (rtn_u64)c * RTN_CT_CHUNK + pre[q] + (rtn_u32)__popcll(m & lane_lt);
+    f.r[u] = (rtn_u64)c * RTN_CT_CHUNK + pre[u] + (rtn_u32)__popcll(m & lane_lt);
     f.frame[u] = (c * (RTN_CT_CHUNK / 64u) + q) * 64u + lane;
 #pragma unroll
     for (int j = 0; j < 6; ++j) f.rec[u][j] = 0u;
-    f.cv[u] = 0ull;
-    if (f.has[u]) {
-      // streamed once: non-temporal, so the occupancy bitmap keeps its place in L2
-      const rtn_u64* rp = reinterpret_cast<const rtn_u64*>(a.recs + f.r[u] * 6u);  // 8-byte aligned
-#pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        const rtn_u64 x = __builtin_nontemporal_load(rp + j);
-        f.rec[u][2 * j] = (rtn_u32)x;
-        f.rec[u][2 * j + 1] = (rtn_u32)(x >> 32);
-      }
-      f.cv[u] = __builtin_nontemporal_load(a.conn + f.r[u]);
-    }
+    // streamed once: non-temporal, so the occupancy bitmap keeps its place in L2. The record
+    // itself is read only by frames that need their key (rtn_ct_load_rec): rtn_conn_t carries
+    // the IPv6 and UDP bits the rest needs.
+    f.cv[u] = f.has[u] ? __builtin_nontemporal_load(a.conn + f.r[u]) : 0ull;
   }
 #pragma unroll
   for (rtn_u32 u = 0; u < G; ++u) {
-    m6[u] = __ballot(f.has[u] && ((f.rec[u][5] >> 7) & 1u));
+    m6[u] = __ballot(f.has[u] && ((f.cv[u] >> 61) & 1ull));  // RTN_CONN_IPV6
     if (lane == 0u) v6cnt[w * G + u] = (rtn_u32)__popcll(m6[u]);
   }
   __syncthreads();
@@ -215,6 +210,17 @@ __device__ __forceinline__ void rtn_ct_load(const rtn_ct_args& a, rtn_ct_frames&
     for (rtn_u32 j = 0; j < q; ++j) v6base += v6cnt[j];
     const rtn_u64 v6r = (rtn_u64)c * RTN_CT_CHUNK + v6base + (rtn_u32)__popcll(m6[u] & lane_lt);
     f.a6[u] = (m6[u] >> lane) & 1ull ? a.addr6 + v6r * 8u : nullptr;
+  }
+}
+
+// The record of group u's frame (for its key).
+__device__ __forceinline__ void rtn_ct_load_rec(const rtn_ct_args& a, rtn_ct_frames& f, rtn_u32 u) {
+  const rtn_u64* rp = reinterpret_cast<const rtn_u64*>(a.recs + f.r[u] * 6u);  // 8-byte aligned
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const rtn_u64 x = __builtin_nontemporal_load(rp + j);
+    f.rec[u][2 * j] = (rtn_u32)x;
+    f.rec[u][2 * j + 1] = (rtn_u32)(x >> 32);
   }
 }
 
@@ -232,11 +238,14 @@ extern "C" __global__ void __launch_bounds__(RTN_CT_BLOCK) rtn_ct_insert(rtn_ct_
   for (rtn_u32 u = 0; u < G; ++u) {
     // openers: creates, and not a TCP opener dropped by filter_first_packet
     const rtn_u32 info = (rtn_u32)(f.cv[u] >> 32);
-    const bool tcp = !((f.rec[u][5] >> 6) & 1u);
+    const bool tcp = !((info >> 30) & 1u);  // RTN_CONN_UDP
     active[u] = f.has[u] && ((info >> 26) & 1u) && !(tcp && (info & 0x3ffffffu) == 0u);
-    if (active[u]) rtn_ct_make_key(a, f.rec[u], f.cv[u], f.a6[u], k[u]);
+    if (active[u]) rtn_ct_load_rec(a, f, u);
     slot[u] = (rtn_u32)f.cv[u] & a.cap_mask;
   }
+#pragma unroll
+  for (rtn_u32 u = 0; u < G; ++u)
+    if (active[u]) rtn_ct_make_key(a, f.rec[u], f.cv[u], f.a6[u], k[u]);
   // Phase A: find the key or the first empty slot of its probe chain (no writes).
   bool at_empty[G];
 #pragma unroll
@@ -378,6 +387,12 @@ extern "C" __global__ void __launch_bounds__(RTN_CT_BLOCK) rtn_ct_lookup(rtn_ct_
       s1[u] = sp[1];
       s2[u] = sp[2];
       s3[u] = reinterpret_cast<const uint2*>(sp + 3)[0];
+      rtn_ct_load_rec(a, f, u);
+    }
+  }
+#pragma unroll
+  for (rtn_u32 u = 0; u < G; ++u) {
+    if (occ0[u]) {
       rtn_ct_make_key(a, f.rec[u], f.cv[u], f.a6[u], k[u]);
       t[u] = (rtn_u64)s0[u].x | ((rtn_u64)s0[u].y << 32);
     }
@@ -388,7 +403,7 @@ extern "C" __global__ void __launch_bounds__(RTN_CT_BLOCK) rtn_ct_lookup(rtn_ct_
     const rtn_u64 cv = f.cv[u];
     const rtn_u32 info = (rtn_u32)(cv >> 32), frame = f.frame[u];
     const bool opens = (info >> 26) & 1u;
-    const bool dropped = !((f.rec[u][5] >> 6) & 1u) && (info & 0x3ffffffu) == 0u;
+    const bool dropped = !((info >> 30) & 1u) && (info & 0x3ffffffu) == 0u;  // TCP opener the filter drops
     rtn_u32 slot = (rtn_u32)cv & a.cap_mask, status = 0u, found = 0xffffffffu;
     if (occ0[u] && t[u] == k[u].fp) {
       const rtn_u32 w[10] = {s1[u].x, s1[u].y, s1[u].z, s1[u].w, s2[u].x, s2[u].y, s2[u].z, s2[u].w, s3[u].x, s3[u].y};

@@ -508,7 +508,8 @@ __device__ __forceinline__ void rtn_group(const rtn_args& a, rtn_u32 g, rtn_u32 
 #pragma unroll
       for (int j = 0; j < RTN_CM_WORDS; ++j) anyc |= cm[j];
       const rtn_u32 info = (pdata & 0x1fffu) | ((pterm & 0x1fffu) << 13) | (creates ? 1u << 26 : 0u) |
-                           (gt ? 1u << 27 : 0u) | (anyc ? 1u << 28 : 0u);
+                           (gt ? 1u << 27 : 0u) | (anyc ? 1u << 28 : 0u) | (v.v6 ? 1u << 29 : 0u) |
+                           (tcp ? 0u : 1u << 30);
       cring[r & (RTN_RING - 1u)] = (rtn_u64)h | ((rtn_u64)info << 32);
 #if RTN_CONN_WORDS > 0
 #pragma unroll
@@ -795,6 +796,7 @@ struct rtn_pd_args {
   const rtn_u64* fwd_bm;
   const rtn_l4rec* recs;
   const unsigned char* addr6;
+  const rtn_u64* conn;         // rtn_conn_t, indexed like recs (its IPv6 bit gives the addr6 rank)
   const rtn_u32* ct;           // rtn_ct_entry_t {slot, status}, indexed like recs
   const unsigned short* dlen;
   const rtn_u32* state;        // [state_slots][1 + RTN_PD_FACTS]: flags (bit 0: PacketDeliver), facts
@@ -835,7 +837,7 @@ extern "C" __global__ void __launch_bounds__(RTN_PD_THREADS) rtn_pd_kernel(rtn_p
     for (rtn_u32 u = 0; u < G; ++u) pre[u] += j < w * G + u ? pj : 0u;
   }
   bool has[G];
-  rtn_u64 r[G];
+  rtn_u64 r[G], cv[G];
   rtn_u32 rec[G][6], slot[G], st[G];
 #pragma unroll
   for (rtn_u32 u = 0; u < G; ++u) {
@@ -847,17 +849,13 @@ extern "C" __global__ void __launch_bounds__(RTN_PD_THREADS) rtn_pd_kernel(rtn_p
     for (int j = 0; j < 6; ++j) rec[u][j] = 0u;
     slot[u] = 0xFFFFFFFFu;
     st[u] = 0u;
+    cv[u] = 0ull;
     if (has[u]) {
-      const rtn_u64* rp = reinterpret_cast<const rtn_u64*>(a.recs + r[u]);
-#pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        const rtn_u64 x = __builtin_nontemporal_load(rp + j);
-        rec[u][2 * j] = (rtn_u32)x;
-        rec[u][2 * j + 1] = (rtn_u32)(x >> 32);
-      }
+      // 16 B per forwarded frame; the 24-B record only for frames that take part (below)
       const rtn_u64 e = __builtin_nontemporal_load(reinterpret_cast<const rtn_u64*>(a.ct) + r[u]);
       slot[u] = (rtn_u32)e;
       st[u] = (rtn_u32)(e >> 32);
+      cv[u] = __builtin_nontemporal_load(a.conn + r[u]);
     }
   }
   // the connection's state row: flags and facts in one go (RTN_CT_HIT | RTN_CT_PRIOR only)
@@ -872,13 +870,20 @@ extern "C" __global__ void __launch_bounds__(RTN_PD_THREADS) rtn_pd_kernel(rtn_p
       const rtn_u32* sp = a.state + (rtn_u64)slot[u] * (1u + RTN_PD_FACTS);
 #pragma unroll
       for (int j = 0; j <= RTN_PD_FACTS; ++j) sv[u][j] = sp[j];
+      const rtn_u64* rp = reinterpret_cast<const rtn_u64*>(a.recs + r[u]);
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const rtn_u64 x = __builtin_nontemporal_load(rp + j);
+        rec[u][2 * j] = (rtn_u32)x;
+        rec[u][2 * j + 1] = (rtn_u32)(x >> 32);
+      }
     }
   }
   // IPv6 records are dense per chunk in addr6: rank among the chunk's IPv6 records
   rtn_u64 m6[G];
 #pragma unroll
   for (rtn_u32 u = 0; u < G; ++u) {
-    m6[u] = __ballot(has[u] && ((rec[u][5] >> 7) & 1u));
+    m6[u] = __ballot(has[u] && ((cv[u] >> 61) & 1ull));  // RTN_CONN_IPV6
     if (lane == 0u) v6n[w * G + u] = (rtn_u32)__popcll(m6[u]);
   }
   __syncthreads();

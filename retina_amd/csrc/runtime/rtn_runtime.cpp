@@ -211,6 +211,7 @@ struct PdArgs {
   const uint64_t* fwd_bm;
   const rtn_l4ctx_t* recs;
   const uint8_t* addr6;
+  const rtn_conn_t* conn;
   const rtn_ct_entry_t* ct;
   const uint16_t* dlen;
   const uint32_t* state;
@@ -478,7 +479,8 @@ int32_t rtn_pd_run(rtn_pc_t* pc, const rtn_pc_out_t* out, const rtn_ct_entry_t* 
                    void* stream) {
   if (!pc || !out || !ct || !data_len || !pd_bitmap) return fail(RTN_EINVAL, "null argument");
   if (n == 0) return RTN_OK;
-  if (!out->fwd_bitmap || !out->l4 || !out->addr6) return fail(RTN_EINVAL, "fwd_bitmap, l4 and addr6 required");
+  if (!out->fwd_bitmap || !out->l4 || !out->addr6 || !out->conn)
+    return fail(RTN_EINVAL, "fwd_bitmap, l4, addr6 and conn required");
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (pc->program->prog.pd_stmts.empty()) {  // no packet-level subscription: nothing is delivered
     hipError_t e = hipMemsetAsync(pd_bitmap, 0, rtn_out_bitmap_bytes(n), s);
@@ -489,6 +491,7 @@ int32_t rtn_pd_run(rtn_pc_t* pc, const rtn_pc_out_t* out, const rtn_ct_entry_t* 
   a.fwd_bm = out->fwd_bitmap;
   a.recs = out->l4;
   a.addr6 = out->addr6;
+  a.conn = out->conn;
   a.ct = ct;
   a.dlen = data_len;
   a.state = state;

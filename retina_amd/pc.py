@@ -400,8 +400,8 @@ def pd_run(pc: "PacketContinue", pc_out: PCOutputs, ct_entries, data_len, state,
     tensors: counts [record][n_pd_stmts] uint32 (valid where the bitmap is set)."""
     import torch
 
-    if pc_out.addr6 is None:
-        raise RetinaError(-22, "pd_run needs outputs allocated with addr6=True")
+    if pc_out.addr6 is None or pc_out.conn is None:
+        raise RetinaError(-22, "pd_run needs outputs allocated with addr6=True and conn=True")
     n = pc_out.n
     L = lib()
     dev = torch.device("cuda", pc.device)
