@@ -53,6 +53,13 @@ int32_t rtn_pd_run(rtn_pc_t* pc, const rtn_pc_out_t* out, const rtn_ct_entry_t* 
                    void* stream);
 size_t rtn_out_pd_counts_bytes(uint32_t n, uint32_t n_pd_stmts);
 
+/* The callback sequence (statement indices, in the order the generated packet_deliver runs them)
+ * of one delivering frame, from its counts row and its connection's facts: statements inside one
+ * session loop run together once per matching session. *n = the sequence length; RTN_ERANGE
+ * (with *n set) if it exceeds cap. */
+int32_t rtn_program_pd_replay(const rtn_program_t* p, const uint32_t* counts, const uint32_t* facts, uint32_t* out,
+                              uint32_t cap, uint32_t* n);
+
 #ifdef __cplusplus
 }
 #endif

@@ -332,6 +332,39 @@ size_t rtn_program_pd_rust(const rtn_program_t* p, char* buf, size_t cap) {
   return p ? copy_text(p->prog.rust_pd_listing, buf, cap) : 0;
 }
 
+// The callback order of one frame from its counts: statements of one session-loop body repeat as
+// a block, facts[fact] times (deliver_filter.rs:123-151); a statement fires in a pass iff its
+// count is non-zero. Recursion over the loop nesting of consecutive statements.
+static size_t pd_replay_rec(const std::vector<rtn::PdStmt>& st, const uint32_t* counts, const uint32_t* facts,
+                            size_t b, size_t e, size_t depth, uint32_t* out, size_t cap, size_t n) {
+  size_t i = b;
+  while (i < e) {
+    if (st[i].loops.size() == depth) {
+      if (counts[i]) {
+        if (n < cap && out) out[n] = (uint32_t)i;
+        ++n;
+      }
+      ++i;
+      continue;
+    }
+    const uint32_t node = st[i].loops[depth].first, fact = st[i].loops[depth].second;
+    size_t j = i;
+    while (j < e && st[j].loops.size() > depth && st[j].loops[depth].first == node) ++j;
+    for (uint32_t r = 0; r < facts[fact]; ++r) n = pd_replay_rec(st, counts, facts, i, j, depth + 1, out, cap, n);
+    i = j;
+  }
+  return n;
+}
+
+int32_t rtn_program_pd_replay(const rtn_program_t* p, const uint32_t* counts, const uint32_t* facts, uint32_t* out,
+                              uint32_t cap, uint32_t* n) {
+  if (!p || !counts || !n || (!facts && !p->prog.pd_facts.empty())) return fail(RTN_EINVAL, "null argument");
+  const size_t k = pd_replay_rec(p->prog.pd_stmts, counts, facts, 0, p->prog.pd_stmts.size(), 0, out, cap, 0);
+  *n = (uint32_t)k;
+  if (k > cap) return fail(RTN_ERANGE, "replay longer than the output capacity (*n holds the length)");
+  return RTN_OK;
+}
+
 int32_t rtn_program_conn_table(const rtn_program_t* p, uint32_t* sub_ids, uint8_t* kinds, uint32_t cap) {
   if (!p) return fail(RTN_EINVAL, "null program");
   const auto& d = p->prog.conn_delivers;

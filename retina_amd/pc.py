@@ -92,6 +92,8 @@ EXPORTS = {
     "rtn_pd_run": (C.c_int32, [C.c_void_p, C.POINTER(_Out), C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p,
                                C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p]),
     "rtn_out_pd_counts_bytes": (C.c_size_t, [C.c_uint32, C.c_uint32]),
+    "rtn_program_pd_replay": (C.c_int32, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
+                                          C.POINTER(C.c_uint32)]),
     # include/retina_ingest.h
     "rtn_pcap_open": (C.c_int32, [C.c_char_p, C.c_uint32, C.POINTER(C.c_void_p)]),
     "rtn_pcap_next_batch": (C.c_int32, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint32,
@@ -238,6 +240,17 @@ class Program:
         import json
 
         return json.loads(_text(lib().rtn_program_pd_json, self._h))
+
+    def pd_replay(self, counts_row, facts_row) -> list[int]:
+        """rtn_program_pd_replay: one frame's callback sequence from its counts and facts."""
+        c = np.ascontiguousarray(counts_row, np.uint32)
+        f = np.ascontiguousarray(facts_row, np.uint32)
+        n = C.c_uint32()
+        lib().rtn_program_pd_replay(self._h, c.ctypes.data, f.ctypes.data if f.size else None, None, 0, C.byref(n))
+        out = np.zeros(max(n.value, 1), np.uint32)
+        _check(lib().rtn_program_pd_replay(self._h, c.ctypes.data, f.ctypes.data if f.size else None,
+                                           out.ctypes.data, n.value, C.byref(n)))
+        return out[:n.value].tolist()
 
     def tree_json(self, layer: int) -> dict:
         """Collapsed tree of layer 0 (PacketContinue), 1 (Packet) or 2 (PacketDeliver) as nested dicts."""

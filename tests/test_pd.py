@@ -162,7 +162,7 @@ def test_pd_oracle_hand_checked():
 
 
 def test_pd_replay_reproduces_loop_interleaving():
-    _, pd, df = _setup()
+    prog, pd, df = _setup()
     rng = np.random.default_rng(2)
     for _ in range(300):
         facts = rng.integers(0, 4, len(pd["facts"]))
@@ -178,6 +178,7 @@ def test_pd_replay_reproduces_loop_interleaving():
         seq = df.evaluate(f, len(f), facts)
         counts = np.bincount(np.array(seq, np.int64), minlength=len(pd["stmts"]))
         assert pc.pd_replay(pd, counts, facts) == seq
+        assert prog.pd_replay(counts, facts) == seq  # the C ABI's replay (rtn_program_pd_replay)
 
 
 def _pd_pool(rng, n):
