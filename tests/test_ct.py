@@ -161,3 +161,36 @@ def test_ct_rebuild_moves_connections(gpu):
     frames = helpers.flow_frames(rng, pool, 4000, p_syn=0.2)
     _check(r.batch(frames), model.process(_model_frames(frames, r.pf)), ids, owner)
     assert r.ct.stats()["live"] == len(model.present)
+
+
+@pytest.mark.gpu
+def test_ct_large_batch_properties(gpu):
+    """At 2^21 cfg2 frames (size-independent properties, no per-frame model): a second pass over
+    the same batch finds every connection the first pass opened, as a prior one; frames that
+    could not open one still miss; one slot per opening frame; live = openers."""
+    import torch
+
+    from retina_amd import synth
+
+    n = 1 << 21
+    slab, dlen = synth.cfg2(n, start=77)
+    prog = pc.Program.from_spec(SETS["cfg2"])
+    ctx = pc.PacketContinue(prog, 0)
+    dev = torch.device("cuda", 0)
+    out = ctx.alloc_outputs(n, conn=True)
+    ctx.run(torch.from_numpy(slab).to(dev), 64, torch.from_numpy(dlen.view(np.int16)).to(dev), n, out)
+    ct = pc.ConnTable(0, 23)
+    e1 = pc.decode_ct(ct.process(out), out)
+    e2 = pc.decode_ct(ct.process(out), out)
+    torch.cuda.synchronize()
+    s1, s2 = e1[:, 1], e2[:, 1]
+    assert len(e1) == int(out.decode()["fwd"].sum()) > n // 8
+    assert not np.isin(s1 & 0xFF, [pc.CT_FULL, pc.CT_COLLISION]).any()
+    new = s1 == pc.CT_NEW
+    assert new.any() and (s1 == pc.CT_MISS).any()
+    # synthetic 5-tuples are unique: every opener opens its own connection, in its own slot
+    assert len(np.unique(e1[new, 0])) == int(new.sum()) == ct.stats()["live"]
+    assert (s2[new] == (pc.CT_HIT | pc.CT_PRIOR)).all() and (e2[new, 0] == e1[new, 0]).all()
+    assert (s2[s1 == pc.CT_MISS] == pc.CT_MISS).all()
+    assert (s2[s1 == pc.CT_NEW_DROPPED] == pc.CT_NEW_DROPPED).all()
+    assert ct.stats()["live"] == int(new.sum())
