@@ -141,7 +141,7 @@ __device__ __forceinline__ rtn_u64* rtn_ct_tag(const rtn_ct_args& a, rtn_u32 slo
 }
 
 #ifndef RTN_CT_GPW
-#define RTN_CT_GPW 4u  // 64-frame groups per wave: a chunk is one block of 8 / RTN_CT_GPW waves
+#define RTN_CT_GPW 2u  // 64-frame groups per wave (cfg2 steady pass: 1 -> 0.62, 2 -> 0.52, 4 -> 0.62, 8 -> 1.13 ms)
 #endif
 #define RTN_CT_BLOCK (64u * (RTN_CT_CHUNK / 64u) / RTN_CT_GPW)
 

@@ -197,14 +197,16 @@ struct KArgs {
   uint64_t* conn_dlv;
 };
 
-// RTN_PD_GPW of the kernel (pc_kernel.hip; an RTN_KERNEL_DEFINES experiment may override it)
-uint32_t pd_groups_per_wave() {
-  const std::string d = env_defines();
-  size_t at = d.find("#define RTN_PD_GPW ");
-  if (at == std::string::npos) return 1u;
-  uint32_t g = (uint32_t)strtoul(d.c_str() + at + 19, nullptr, 10);
-  return (g == 1u || g == 2u || g == 4u || g == 8u) ? g : 1u;
+// Groups per wave of a kernel (RTN_PD_GPW / RTN_CT_GPW): the default, unless an RTN_KERNEL_DEFINES
+// experiment overrides it (the launch's block size follows it).
+uint32_t groups_per_wave(const char* name, uint32_t dflt) {
+  const std::string d = env_defines(), key = std::string("#define ") + name + " ";
+  size_t at = d.find(key);
+  if (at == std::string::npos) return dflt;
+  uint32_t g = (uint32_t)strtoul(d.c_str() + at + key.size(), nullptr, 10);
+  return (g == 1u || g == 2u || g == 4u || g == 8u) ? g : dflt;
 }
+uint32_t pd_groups_per_wave() { return groups_per_wave("RTN_PD_GPW", 1u); }
 
 // must match struct rtn_pd_args in pc_kernel.hip
 struct PdArgs {
@@ -582,7 +584,7 @@ struct rtn_ct {
 };
 
 namespace {
-constexpr uint32_t RTN_CT_GPW = 4;  // must match ct_kernel.hip
+constexpr uint32_t RTN_CT_GPW = 2;  // must match ct_kernel.hip
 
 struct CtArgs {  // must match struct rtn_ct_args in ct_kernel.hip
   const uint64_t* fwd_bm;
@@ -702,7 +704,7 @@ int32_t rtn_ct_process(rtn_ct_t* ct, const rtn_pc_out_t* pc, uint32_t n, rtn_ct_
   a.check = spread ? 0u : 1u;
   const uint32_t chunks = (n + RTN_CHUNK_FRAMES - 1u) / RTN_CHUNK_FRAMES;  // one 512-thread block each
   void* p[] = {&a};
-  const uint32_t threads = 512u / RTN_CT_GPW;  // ct_kernel.hip: a chunk per block, RTN_CT_GPW groups per wave
+  const uint32_t threads = 512u / groups_per_wave("RTN_CT_GPW", RTN_CT_GPW);  // a chunk per block
   hipError_t e = hipModuleLaunchKernel(ct->insert, chunks, 1, 1, threads, 1, 1, 0, s, p, nullptr);
   if (e != hipSuccess) return hip_fail("rtn_ct_insert", e);
   e = hipModuleLaunchKernel(ct->lookup, chunks, 1, 1, threads, 1, 1, 0, s, p, nullptr);
