@@ -2,8 +2,10 @@
 // consecutive packets (a "group"). The filter compiler splices a tree-specialised `rtn_filter` at
 // the RTN_FILTER marker below (the analogue of filtergen's generated `packet_continue`), and the
 // whole translation unit is compiled once per subscription set (hiprtc at rtn_pc_create, or
-// hipcc --genco ahead of time). It holds two kernels: rtn_pc_kernel_s64 for 64-byte slots and
-// rtn_pc_kernel for any larger stride (a multiple of 64).
+// hipcc --genco ahead of time). It holds the packet-stage kernels -- rtn_pc_kernel_s64 for 64-byte
+// slots, rtn_pc_kernel_split for 64-byte head slots + 64-byte ext slots, rtn_pc_kernel for any
+// larger stride (a multiple of 64) -- and rtn_pd_kernel, the PacketDeliver filter (rtn_pd_run),
+// whose generated tree (RTN_PD_FILTER marker) comes from the same program.
 //
 // Per packet it reproduces, bit for bit:
 //   * Mbuf::get_data bounds (core/src/memory/mbuf.rs:125-135): offset < data_len && offset+size <= data_len
