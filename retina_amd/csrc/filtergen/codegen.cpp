@@ -364,6 +364,56 @@ struct Gen {
     }
   }
 
+
+  // ---- FilterLayer::Packet (packet_filter) as straight-line HIP, like pc_flat: actions with
+  // their terminal half and statement-mask bits under each node's reach flag. Statement
+  // numbering follows children() / update_body_conn().
+  uint32_t flat_conn_stmt = 0;
+  void conn_flat_body(const PNode& n, const std::string& R) {
+    if (!n.actions.drop())
+      hip += "  data |= " + R + " ? " + u32lit(n.actions.data) + " : 0u; term |= " + R + " ? " +
+             u32lit(n.actions.terminal) + " : 0u;\n";
+    auto stmt = [&](uint32_t sub) {
+      uint32_t k = flat_conn_stmt++;
+      if (k >= prog.conn_delivers.size() || prog.conn_delivers[k].sub_id != sub)
+        throw FilterError("internal: packet-filter statement order");
+      hip += "  cm[" + std::to_string(k / 64) + "] |= " + R + " ? (1ull << " + std::to_string(k % 64) + ") : 0ull;\n";
+    };
+    for (auto& dv : n.deliver) stmt((uint32_t)dv.id);
+    for (auto& sv : n.stream) stmt((uint32_t)sv.id);
+  }
+  void conn_flat(const PNode& n, const std::string& R) {
+    bool first_unary = true;
+    std::string T;
+    for (auto& c : n.children) {
+      if (!c.pred.on_packet()) continue;
+      const std::string id = std::to_string(c.id);
+      std::string cond;
+      bool is_else;
+      if (c.pred.is_unary()) {
+        const std::string& proto = c.pred.protocol;
+        cond = proto == "ipv4" ? "c.v4" : proto == "ipv6" ? "c.v6" : proto == "tcp" ? "c.tcp" : "c.udp";
+        is_else = !first_unary;
+        first_unary = false;
+      } else {
+        cond = binary(c.pred).first;
+        is_else = c.if_else;
+      }
+      const std::string rc = "r" + id;
+      hip += "  const bool k" + id + " = " + cond + ";\n";
+      if (!is_else || T.empty()) {
+        T = "t" + id;
+        hip += "  bool " + T + " = k" + id + ";\n";
+        hip += "  const bool " + rc + " = " + R + " && k" + id + ";\n";
+      } else {
+        hip += "  const bool " + rc + " = " + R + " && !" + T + " && k" + id + ";\n";
+        hip += "  " + T + " = " + T + " || k" + id + ";\n";
+      }
+      conn_flat(c, rc);
+      conn_flat_body(c, rc);
+    }
+  }
+
   // ---- FilterLayer::PacketDeliver (deliver_filter.rs) ----
   // The body multiplies `m` (how many times the enclosing session loops run it) into per-statement
   // counts; `f` holds the connection's facts (PdFact) and `pok` the Payload guard.
@@ -602,6 +652,10 @@ PacketProgram compile_packet_program(const std::vector<SubscriptionSpec>& subs) 
   for (auto& c : croot.children) c_any_pkt = c_any_pkt || c.pred.on_packet();
   if (!croot.actions.drop() || !croot.deliver.empty()) gc.update_body(croot, 1);  // packet_filter.rs:15-17
   gc.children(croot, 1);
+  gc.hip.clear();
+  if (!croot.actions.drop() || !croot.deliver.empty()) gc.conn_flat_body(croot, "true");
+  gc.conn_flat(croot, "true");
+  if (gc.flat_conn_stmt != prog.conn_delivers.size()) throw FilterError("internal: packet-filter statement count");
   prog.hip_conn_body =
       "__device__ __forceinline__ void rtn_conn_filter(const rtn_cview& c, rtn_u32& data, rtn_u32& term, rtn_u64* cm) "
       "{\n  (void)c; (void)cm;\n" + gc.hip + "}\n";
