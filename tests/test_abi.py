@@ -72,3 +72,28 @@ def test_output_sizes():
     assert L.rtn_out_l4_bytes(1025) == 1536 * 24
     assert L.rtn_out_addr6_bytes(1) == 512 * 32
     assert L.rtn_out_dlv_bytes(64, 2) == 512 * 3 * 8
+
+
+def test_headers_are_c(tmp_path):
+    """include/*.h are plain C: a C11 translation unit including all of them compiles with gcc
+    -Wall -Wextra -Werror, and links against libretina_pc.so (every declared symbol resolves)."""
+    import re
+    import subprocess
+
+    inc = Path(__file__).resolve().parent.parent / "include"
+    lib = Path(pc.__file__).resolve().parent / "_lib"
+    names = set()
+    for h in HEADERS:
+        names |= set(re.findall(r"^\s*(?:[\w\s\*]+?)\b(rtn_\w+)\s*\(", h.read_text(), re.M))
+    src = "".join(f'#include "{h.name}"\n' for h in HEADERS)
+    src += "#include <stdio.h>\nint main(void) {\n"
+    src += "".join(f'  printf("%p\\n", (void*)&{n});\n' for n in sorted(names))
+    src += "  return 0;\n}\n"
+    c = tmp_path / "abi.c"
+    c.write_text(src)
+    exe = tmp_path / "abi"
+    r = subprocess.run(["gcc", "-std=c11", "-Wall", "-Wextra", "-Werror", f"-I{inc}", str(c),
+                        "-o", str(exe), f"-L{lib}", "-lretina_pc", f"-Wl,-rpath,{lib}",
+                        "-L/opt/rocm/lib", "-Wl,-rpath,/opt/rocm/lib"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    assert len(names) > 40
