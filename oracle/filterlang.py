@@ -1,4 +1,5 @@
-"""ORACLE (test infrastructure only): Retina's filter language and PacketContinue predicate tree.
+"""ORACLE (test infrastructure only): Retina's filter language and its packet-side predicate trees
+(PacketContinue, Packet, PacketDeliver).
 
 Restates, in plain Python:
   core/src/filter/grammar.pest:5-75       the PEG (pest 2.5: ordered choice, greedy repetition,
@@ -15,7 +16,12 @@ Restates, in plain Python:
   datatypes/src/typedefs.rs:15-86         DATATYPES levels
   filtergen/src/lib.rs:241-261            filter_subtree
   filtergen/src/packet_filter.rs, utils.rs:18-379, data.rs:262-331   generated packet_continue
-Only the PacketContinue layer is restated here; the other layers are out of scope.
+  core/src/filter/ptree.rs:641-748         prune_packet_conditions / prune_redundant_branches
+                                           (FilterLayer::Packet and PacketDeliver, ConnTree /
+                                           DeliverTree below)
+  core/src/filter/datatypes.rs:108-345, 563-637  DataType flags, packet_filter actions,
+                                           should_deliver / should_stream at the Packet layer
+The Protocol, Session and ConnectionDeliver layers run on the host and are not restated.
 """
 from __future__ import annotations
 
