@@ -588,6 +588,9 @@ struct Gen {
 
 }  // namespace
 
+// Trees up to this many nodes are emitted straight-line (cfg4's 127-node tree: -8 % kernel time).
+constexpr size_t kFlatMaxNodes = 256;
+
 PacketProgram compile_packet_program(const std::vector<SubscriptionSpec>& subs) {
   PacketProgram prog;
   prog.subs = subs;
@@ -641,6 +644,9 @@ PacketProgram compile_packet_program(const std::vector<SubscriptionSpec>& subs) 
   prog.hip_body = "__device__ __forceinline__ void rtn_filter(const rtn_view& v, rtn_u32& act, rtn_u64* dm) {\n"
                   "  (void)v; (void)dm;\n" +
                   g.hip + "}\n";
+  // The straight-line form evaluates every node for every frame; the nested form skips subtrees
+  // no lane of a wave enters. Past kFlatMaxNodes the second wins (large disjoint subtrees).
+  if (prog.tree.size > kFlatMaxNodes) prog.hip_body = prog.hip_body_branchy;
   prog.rust_listing = "let mut result = Actions::new();\n" + g.rust + "result\n";
 
   // packet_filter: the same emission (gen_packet_filter with FilterLayer::Packet), evaluated on a
@@ -652,10 +658,12 @@ PacketProgram compile_packet_program(const std::vector<SubscriptionSpec>& subs) 
   for (auto& c : croot.children) c_any_pkt = c_any_pkt || c.pred.on_packet();
   if (!croot.actions.drop() || !croot.deliver.empty()) gc.update_body(croot, 1);  // packet_filter.rs:15-17
   gc.children(croot, 1);
-  gc.hip.clear();
-  if (!croot.actions.drop() || !croot.deliver.empty()) gc.conn_flat_body(croot, "true");
-  gc.conn_flat(croot, "true");
-  if (gc.flat_conn_stmt != prog.conn_delivers.size()) throw FilterError("internal: packet-filter statement count");
+  if (prog.conn_tree.size <= kFlatMaxNodes) {
+    gc.hip.clear();
+    if (!croot.actions.drop() || !croot.deliver.empty()) gc.conn_flat_body(croot, "true");
+    gc.conn_flat(croot, "true");
+    if (gc.flat_conn_stmt != prog.conn_delivers.size()) throw FilterError("internal: packet-filter statement count");
+  }
   prog.hip_conn_body =
       "__device__ __forceinline__ void rtn_conn_filter(const rtn_cview& c, rtn_u32& data, rtn_u32& term, rtn_u64* cm) "
       "{\n  (void)c; (void)cm;\n" + gc.hip + "}\n";

@@ -9,7 +9,7 @@ import pytest
 
 import helpers
 from golden.filter_sets import SETS
-from retina_amd import synth
+from retina_amd import pc, synth
 
 GOLD = Path(__file__).resolve().parent / "golden"
 pytestmark = pytest.mark.gpu
@@ -119,3 +119,27 @@ def test_full_size_cfg2_properties(gpu):
     sel = (l4["pkt_idx"] >= lo) & (l4["pkt_idx"] < lo + (1 << 16))
     assert np.array_equal(l4["pkt_idx"][sel] - lo, ora["rec"]["idx"])
     assert np.array_equal(l4["seq_no"][sel], ora["rec"]["seq"])
+
+
+def test_large_tree_uses_nested_form_and_matches(gpu):
+    """Trees past the straight-line threshold are emitted as nested if/else (codegen.cpp
+    kFlatMaxNodes): 300 packet-level port subscriptions (a 600-node tree) plus packet-level
+    callbacks, on IMIX frames whose ports hit them."""
+    subs = [(f"tcp.dst_port = {1000 + k} or udp.src_port = {2000 + k}", ["ConnRecord"], f"c{k}") for k in range(300)]
+    subs += [("tcp.port = 1007", ["ZcFrame"], "z"), ("udp.port >= 2290", ["Payload"], "p")]
+    spec = synth._toml(subs)
+    prog = pc.Program.from_spec(spec)
+    assert prog.info["tree_size"] > 256
+    body = prog.source.split("void rtn_filter(")[1][:300]
+    assert "if (" in body and "const bool k" not in body
+    rng = np.random.default_rng(21)
+    frames = []
+    for j in range(6000):
+        proto = 6 if rng.random() < 0.6 else 17
+        port = int(rng.choice([1000 + int(rng.integers(0, 320)), 2000 + int(rng.integers(0, 320)), int(rng.integers(1, 65536))]))
+        sp, dp = (int(rng.integers(1, 65536)), port) if rng.random() < 0.5 else (port, int(rng.integers(1, 65536)))
+        frames.append(helpers.build_frame(bool(rng.random() < 0.3), int(rng.integers(0, 1 << 32)),
+                                          int(rng.integers(0, 1 << 32)), sp, dp, proto, 0x18,
+                                          payload=bytes(int(rng.integers(0, 5)))))
+    slab, dlen = pc.pack_frames(frames, 128)
+    helpers.assert_same(helpers.gpu_run(spec, slab, 128, dlen), helpers.oracle_run(spec, slab, 128, dlen), "large tree")
