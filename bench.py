@@ -124,36 +124,36 @@ def load_traffic(cfg: str, n: int):
     return None
 
 
-def e2e_rate(ctx, slab: np.ndarray, dlen: np.ndarray, stride: int, dev) -> dict:
+def e2e_rate(ctx, slab: np.ndarray, dlen: np.ndarray, stride: int, dev, chunk: int = 1 << 21,
+             nstreams: int = 4) -> dict:
     """End-to-end rate from pinned host memory: H2D of the header slab + data_len, the kernel,
-    D2H of the bitmaps and L4Context records, pipelined over chunks on two streams."""
+    D2H of the bitmaps and L4Context records, pipelined over chunks on `nstreams` streams."""
     import torch
 
     n = len(dlen)
-    chunk = 1 << 22
     h_slab = torch.from_numpy(slab).pin_memory()
     h_dlen = torch.from_numpy(dlen.view(np.int16)).pin_memory()
-    streams = [torch.cuda.Stream(dev) for _ in range(2)]
+    streams = [torch.cuda.Stream(dev) for _ in range(nstreams)]
     bufs = []
-    for _ in range(2):
+    for _ in range(nstreams):
         bufs.append((torch.empty(chunk * stride, dtype=torch.uint8, device=dev),
                      torch.empty(chunk, dtype=torch.int16, device=dev), ctx.alloc_outputs(chunk, addr6=False, counters=False)))
-    h_out = [torch.empty(bufs[0][2].l4.numel(), dtype=torch.uint8).pin_memory() for _ in range(2)]
-    h_bm = [torch.empty(bufs[0][2].pc_bitmap.numel() * 2, dtype=torch.uint8).pin_memory() for _ in range(2)]
+    h_out = [torch.empty(bufs[0][2].l4.numel(), dtype=torch.uint8).pin_memory() for _ in range(nstreams)]
+    h_bm = [torch.empty(bufs[0][2].pc_bitmap.numel() * 2, dtype=torch.uint8).pin_memory() for _ in range(nstreams)]
 
     def one_pass():
         for k, s in enumerate(range(0, n, chunk)):
             m = min(chunk, n - s)
-            st = streams[k % 2]
-            d_slab, d_dlen, out = bufs[k % 2]
+            st = streams[k % nstreams]
+            d_slab, d_dlen, out = bufs[k % nstreams]
             with torch.cuda.stream(st):
                 d_slab[:m * stride].copy_(h_slab[s * stride:(s + m) * stride], non_blocking=True)
                 d_dlen[:m].copy_(h_dlen[s:s + m], non_blocking=True)
                 ctx.run(d_slab, stride, d_dlen, m, out, stream=st)
-                h_out[k % 2].copy_(out.l4, non_blocking=True)
+                h_out[k % nstreams].copy_(out.l4, non_blocking=True)
                 nb = out.pc_bitmap.numel()
-                h_bm[k % 2][:nb].copy_(out.pc_bitmap, non_blocking=True)
-                h_bm[k % 2][nb:].copy_(out.fwd_bitmap, non_blocking=True)
+                h_bm[k % nstreams][:nb].copy_(out.pc_bitmap, non_blocking=True)
+                h_bm[k % nstreams][nb:].copy_(out.fwd_bitmap, non_blocking=True)
 
     one_pass()
     torch.cuda.synchronize(dev)
@@ -164,8 +164,9 @@ def e2e_rate(ctx, slab: np.ndarray, dlen: np.ndarray, stride: int, dev) -> dict:
     torch.cuda.synchronize(dev)
     dt = (time.perf_counter() - t0) / reps
     return {"mpps": round(n / dt / 1e6, 1), "seconds_per_batch": round(dt, 4), "chunk_frames": chunk,
+            "streams": nstreams,
             "note": "pinned host -> HBM copy of the header slab + data_len, kernel, D2H of bitmaps and L4 records; "
-                    "2 streams; PCIe-bound"}
+                    "PCIe-bound"}
 
 
 # Packet-level subscriptions that match at the protocol/session layer: their packets are
