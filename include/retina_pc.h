@@ -122,8 +122,10 @@ typedef struct rtn_pc_out {
   uint8_t* addr6;        /* optional [ceil(n/512)*512][32]: src|dst of the IPv6 records   */
   uint64_t* dlv_bitmap;  /* [ceil(n/64)] frames with >= 1 packet-level callback (if any)     */
   uint64_t* dlv_records; /* [ceil(n/512)*512][1 + deliver_words]: frame index, statement mask */
-  uint32_t* counters;    /* optional [4]: pc, fwd, dlv totals, status bits; zeroed per run
-                          (NULL: no totals, no memset -- the run is a single kernel launch) */
+  uint32_t* counters;    /* optional [8] (32 B, 8-B aligned): pc, fwd, dlv totals, status bits, then
+                          u64 data_len sum of all frames (TOTAL_BYTE) and u64 data_len sum of the
+                          frames not accepted (IGNORED_BY_PACKET_FILTER_BYTE, rx_core.rs:129-141);
+                          zeroed per run (NULL: no totals, no memset -- one kernel launch) */
   rtn_conn_t* conn;      /* optional [ceil(n/512)*512]: connection stage, indexed like l4       */
   uint64_t* conn_dlv;    /* [ceil(n/512)*512][conn_words] first-packet statement masks; required
                           with conn when the program has first-packet statements           */

@@ -85,7 +85,7 @@ struct rtn_args {
   unsigned char* addr6;       // [ceil(n/64)*64][32] (src, dst) raw bytes, IPv6 records only
   rtn_u64* dlv_bm;            // [ceil(n/64)]  any packet-level delivery
   rtn_u64* dlv_recs;          // [ceil(n/64)*64][1 + RTN_DELIVER_WORDS]  (pkt_idx, statement mask words)
-  rtn_u32* counters;          // [0] pc, [1] fwd, [2] dlv, [3] status bits
+  rtn_u32* counters;          // [0] pc, [1] fwd, [2] dlv, [3] status bits, [4..5] bytes, [6..7] ignored bytes
   const unsigned char* ext;   // split layout: bytes 64..127 of each frame (64-byte slots), or null
   rtn_u64* conn;              // optional [ceil(n/512)*512] rtn_conn_t, indexed like recs (flags bit2)
   rtn_u64* conn_dlv;          // [ceil(n/512)*512][RTN_CONN_WORDS] first-packet statement masks
@@ -272,6 +272,7 @@ __device__ __forceinline__ void rtn_parse(const rtn_u32 (&w)[NW], rtn_u32 dl, rt
 
 struct rtn_acc {
   rtn_u32 pc, fwd, dlv, status;
+  rtn_u64 bytes, ignored;  // this lane's data_len sums: all frames / frames not accepted (rx_core.rs:129-141)
 };
 
 // First 64 B of slot i. Lanes past n re-read the last slot (no branch, no zero fill); their
@@ -437,6 +438,8 @@ __device__ __forceinline__ void rtn_group(const rtn_args& a, rtn_u32 g, rtn_u32 
   const rtn_u32 nfwd = (rtn_u32)__popcll(fwdm);
   acc.pc += (rtn_u32)__popcll(pcm);
   acc.fwd += nfwd;
+  acc.bytes += dl;               // lanes past n have dl == 0
+  acc.ignored += pc ? 0u : dl;
   ch.my_pc = lane == k ? pcm : ch.my_pc;
   ch.my_fwd = lane == k ? fwdm : ch.my_fwd;
 #ifndef RTN_EXP_NO_STORES
@@ -595,7 +598,7 @@ __device__ __forceinline__ void rtn_run(const rtn_args& a) {
   const rtn_u32 nchunks = (nw + RTN_CHUNK_GROUPS - 1u) / RTN_CHUNK_GROUPS;
   const rtn_u64 lane_lt = (lane == 0u) ? 0ull : (~0ull >> (64u - lane));
   constexpr bool slots64 = MODE != RTN_MONO;
-  rtn_acc acc = {0u, 0u, 0u, 0u};
+  rtn_acc acc = {0u, 0u, 0u, 0u, 0ull, 0ull};
   __shared__ __attribute__((aligned(16))) rtn_u64 rtn_ring[4][RTN_RING * 3u];
   rtn_u64* ring = rtn_ring[threadIdx.x >> 6];
   __shared__ __attribute__((aligned(16))) rtn_u64 rtn_cring[4][RTN_RING];  // connection-stage entries
@@ -723,10 +726,18 @@ __device__ __forceinline__ void rtn_run(const rtn_args& a) {
   const rtn_u64 st = __ballot(acc.status != 0u);
   if (lane == 0u && st) atomicOr(&a.counters[3], 1u);
   if (!(a.flags & 2u)) return;
+  rtn_u64 bytes = acc.bytes, ignored = acc.ignored;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    bytes += __shfl_xor(bytes, off);
+    ignored += __shfl_xor(ignored, off);
+  }
   if (lane == 0u) {
     if (acc.pc) atomicAdd(&a.counters[0], acc.pc);
     if (acc.fwd) atomicAdd(&a.counters[1], acc.fwd);
     if (acc.dlv) atomicAdd(&a.counters[2], acc.dlv);
+    if (bytes) atomicAdd(reinterpret_cast<unsigned long long*>(a.counters + 4), bytes);
+    if (ignored) atomicAdd(reinterpret_cast<unsigned long long*>(a.counters + 6), ignored);
   }
 }
 

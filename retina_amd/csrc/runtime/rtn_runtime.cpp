@@ -432,7 +432,7 @@ int32_t rtn_pc_create_from_program(rtn_program_t* p, int device, rtn_pc_t** out)
   if (e != hipSuccess) return fail(RTN_EDEVICE, std::string("hipModuleGetFunction: ") + hipGetErrorString(e));
   e = hipModuleGetFunction(&pc->fn_pd, pc->module, "rtn_pd_kernel");
   if (e != hipSuccess) return fail(RTN_EDEVICE, std::string("hipModuleGetFunction: ") + hipGetErrorString(e));
-  e = hipMalloc(&pc->scratch_counters, 16);
+  e = hipMalloc(&pc->scratch_counters, 32);
   if (e != hipSuccess) return fail(RTN_EDEVICE, std::string("hipMalloc: ") + hipGetErrorString(e));
   if (const char* g = getenv("RTN_GRID")) pc->blocks = (uint32_t)strtoul(g, nullptr, 10);
   *out = pc.release();
@@ -476,7 +476,7 @@ int32_t rtn_pc_run(rtn_pc_t* pc, const rtn_batch_t* in, rtn_pc_out_t* out, void*
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   hipError_t e;
   if (out->counters) {
-    e = hipMemsetAsync(out->counters, 0, 16, s);
+    e = hipMemsetAsync(out->counters, 0, 32, s);
     if (e != hipSuccess) return fail(RTN_EDEVICE, std::string("hipMemsetAsync: ") + hipGetErrorString(e));
   }
   KArgs a;

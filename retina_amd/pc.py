@@ -286,7 +286,13 @@ class PCOutputs:
     conn_words: int = 0
 
     def counters_host(self) -> np.ndarray:
-        return self.counters.cpu().numpy().view(np.uint32)
+        """[pc, fwd, dlv, status] (uint32)."""
+        return self.counters.cpu().numpy().view(np.uint32)[:4]
+
+    def byte_counters_host(self) -> tuple[int, int]:
+        """(data_len sum of all frames, data_len sum of the frames not accepted)."""
+        b = self.counters.cpu().numpy().view(np.uint64)
+        return int(b[2]), int(b[3])
 
     def decode(self) -> dict:
         """Bring results to the host in frame order (numpy)."""
@@ -377,7 +383,7 @@ class PacketContinue:
             addr6=u8(L.rtn_out_addr6_bytes(n)) if addr6 else None,
             dlv_bitmap=u8(L.rtn_out_bitmap_bytes(n)) if dw else None,
             dlv_records=u8(L.rtn_out_dlv_bytes(n, dw)) if dw else None,
-            counters=torch.zeros(16, dtype=torch.uint8, device=dev) if counters else None,
+            counters=torch.zeros(32, dtype=torch.uint8, device=dev) if counters else None,
             deliver_words=dw,
             conn=u8(L.rtn_out_conn_bytes(n)) if conn else None,
             conn_dlv=u8(L.rtn_out_conn_dlv_bytes(n, self.conn_words)) if conn and self.conn_words else None,

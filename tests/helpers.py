@@ -63,6 +63,11 @@ def gpu_run(spec: str, slab: np.ndarray, stride: int, dlen: np.ndarray, device: 
     torch.cuda.synchronize()
     d = out.decode()
     cnt = out.counters_host()
+    # TOTAL_BYTE / IGNORED_BY_PACKET_FILTER_BYTE (rx_core.rs:129-141) from the same launch
+    total, ignored = out.byte_counters_host()
+    dl64 = np.asarray(dlen, np.uint16).astype(np.uint64)
+    assert total == int(dl64.sum()), (total, int(dl64.sum()))
+    assert ignored == int(dl64[~d["pc"][:n]].sum()) if n else ignored == 0
     l4 = d["l4"]
     rec = np.zeros(len(l4), REC)
     for f in ("ver", "proto", "flags", "sport", "dport", "offset", "length"):

@@ -113,6 +113,8 @@ def test_full_size_cfg2_properties(gpu):
     assert np.all(l4["dport"] == 80) and np.all(l4["proto"] == 6) and np.all(l4["ver"] == 4)
     c = out.counters_host()
     assert c[0] == exp.sum() and c[1] == exp.sum() and c[3] == 0
+    total, ignored = out.byte_counters_host()
+    assert total == int(dlen.astype(np.uint64).sum()) and ignored == int(dlen[~exp].astype(np.uint64).sum())
     lo = 3 << 22
     win = slice(lo, lo + (1 << 16))
     ora = helpers.oracle_run(SETS["cfg2"], slab[lo * 64:(lo + (1 << 16)) * 64], 64, dlen[win])
