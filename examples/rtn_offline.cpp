@@ -91,10 +91,12 @@ void walk(const HostSet& h, bool with_ct, Totals& t, FILE* dump) {
   const uint32_t words = (h.n + 63u) / 64u;
   for (uint32_t w = 0; w < words; ++w) t.pc += __builtin_popcountll(h.pcbm[w]);
   for (uint32_t c = 0; c * RTN_CHUNK_FRAMES < h.n; ++c) {
-    uint64_t k = (uint64_t)c * RTN_CHUNK_FRAMES, k6 = k;  // record index, IPv6 address index
+    uint32_t rank = 0;                                // forwarded frames of the chunk before this one
+    uint64_t k6 = (uint64_t)c * RTN_CHUNK_FRAMES;     // IPv6 address index (dense per chunk)
     for (uint32_t w = c * (RTN_CHUNK_FRAMES / 64u); w < (c + 1) * (RTN_CHUNK_FRAMES / 64u) && w < words; ++w) {
-      for (uint64_t b = h.fwd[w]; b; b &= b - 1, ++k) {
+      for (uint64_t b = h.fwd[w]; b; b &= b - 1, ++rank) {
         const uint64_t i = (uint64_t)w * 64u + __builtin_ctzll(b);
+        const uint64_t k = RTN_REC_INDEX(h.n, c, rank);  // record index
         const rtn_l4ctx_t& r = h.l4[k];
         const bool v6 = RTN_L4_IPV6(r.meta);
         ++t.fwd;

@@ -45,7 +45,7 @@ typedef struct rtn_ct rtn_ct_t;
 #define RTN_CT_PRIOR 0x100u   /* flag: the connection existed before this batch                   */
 #define RTN_CT_NO_SLOT 0xFFFFFFFFu
 
-/* Per forwarded frame, indexed like rtn_pc_out_t.l4 (dense per RTN_CHUNK_FRAMES chunk). */
+/* Per forwarded frame, indexed like rtn_pc_out_t.l4 (RTN_REC_INDEX in retina_pc.h). */
 typedef struct rtn_ct_entry {
   uint32_t slot;   /* connection handle, or RTN_CT_NO_SLOT */
   uint32_t status; /* RTN_CT_* | RTN_CT_PRIOR              */

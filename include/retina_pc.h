@@ -109,16 +109,25 @@ typedef struct rtn_batch {
   const uint8_t* ext;       /* split layout: bytes [64, 128) of each frame, 64-byte slots */
 } rtn_batch_t;
 
-/* Record arrays are dense per chunk of RTN_CHUNK_FRAMES frames, in frame order: the k-th
- * forwarded frame of chunk c = i / RTN_CHUNK_FRAMES has its L4Context at l4[c * RTN_CHUNK_FRAMES + k]
- * (k = popcount of fwd_bitmap over the chunk's frames before it); the j-th forwarded IPv6 frame
- * of chunk c (records with RTN_L4_IPV6) has its addresses at addr6[c * RTN_CHUNK_FRAMES + j];
- * dlv_records are ranked by dlv_bitmap the same way. Bitmaps hold bit i % 64 of word i / 64. */
+/* Records are ranked per chunk of RTN_CHUNK_FRAMES frames, in frame order: the k-th forwarded
+ * frame of chunk c = i / RTN_CHUNK_FRAMES (k = popcount of fwd_bitmap over the chunk's frames
+ * before it) has its L4Context at l4[RTN_REC_INDEX(n, c, k)]; conn, conn_dlv, the connection
+ * table's rtn_ct_entry_t and the PacketDeliver counts use the same index. A chunk's records sit
+ * in blocks of RTN_REC_BLOCK, block j of chunk c at block slot j * nchunks + c, so the chunks'
+ * first blocks form one dense stream, their second blocks the next, and so on (the stores of a
+ * partly-forwarded batch stay dense).
+ * The j-th forwarded IPv6 frame of chunk c (records with RTN_L4_IPV6) has its addresses at
+ * addr6[c * RTN_CHUNK_FRAMES + j]; dlv_records are ranked by dlv_bitmap the same way (dense per
+ * chunk). Bitmaps hold bit i % 64 of word i / 64. */
 #define RTN_CHUNK_FRAMES 512u
+#define RTN_REC_BLOCK 64u
+#define RTN_REC_INDEX(n, chunk, k)                                                             \
+  (((uint64_t)((k) / RTN_REC_BLOCK) * (((uint64_t)(n) + RTN_CHUNK_FRAMES - 1u) / RTN_CHUNK_FRAMES) + \
+    (uint64_t)(chunk)) * RTN_REC_BLOCK + (uint64_t)((k) % RTN_REC_BLOCK))
 typedef struct rtn_pc_out {
   uint64_t* pc_bitmap;   /* [ceil(n/64)]  Actions.data contains PacketContinue               */
   uint64_t* fwd_bitmap;  /* [ceil(n/64)]  ... and L4Context::new succeeded (goes to conntrack) */
-  rtn_l4ctx_t* l4;       /* [ceil(n/512)*512] (rtn_out_l4_bytes); unused slots undefined    */
+  rtn_l4ctx_t* l4;       /* [ceil(n/512)*512] (rtn_out_l4_bytes) at RTN_REC_INDEX; unused slots undefined */
   uint8_t* addr6;        /* optional [ceil(n/512)*512][32]: src|dst of the IPv6 records   */
   uint64_t* dlv_bitmap;  /* [ceil(n/64)] frames with >= 1 packet-level callback (if any)     */
   uint64_t* dlv_records; /* [ceil(n/512)*512][1 + deliver_words]: frame index, statement mask */

@@ -168,6 +168,7 @@ __device__ __forceinline__ void rtn_ct_load(const rtn_ct_args& a, rtn_ct_frames&
   const rtn_u32 c = blockIdx.x;
   const rtn_u64 lane_lt = lane ? (~0ull >> (64u - lane)) : 0ull;
   const rtn_u32 nw = (a.n + 63u) / 64u;
+  const rtn_u64 nch = ((rtn_u64)a.n + RTN_CT_CHUNK - 1u) / RTN_CT_CHUNK;
   // the chunk's bitmap words: lane j < 8 holds word j; pre[j] = records before group j
   const rtn_u32 gj = c * (RTN_CT_CHUNK / 64u) + (lane & 7u);
   const rtn_u64 word = gj < nw ? a.fwd_bm[gj] : 0ull;
@@ -188,7 +189,10 @@ __device__ __forceinline__ void rtn_ct_load(const rtn_ct_args& a, rtn_ct_frames&
     const rtn_u32 q = w * G + u;  // group within the chunk
     const rtn_u64 m = __shfl(word, (int)q);
     f.has[u] = c * (RTN_CT_CHUNK / 64u) + q < nw && ((m >> lane) & 1ull);
-    f.r[u] = (rtn_u64)c * RTN_CT_CHUNK + pre[u] + (rtn_u32)__popcll(m & lane_lt);
+    // record slot (RTN_REC_INDEX, retina_pc.h): block k / 64 of chunk c at block slot
+    // (k / 64) * nchunks + c
+    const rtn_u32 k = pre[u] + (rtn_u32)__popcll(m & lane_lt);
+    f.r[u] = ((rtn_u64)(k >> 6) * nch + c) * 64u + (k & 63u);
     f.frame[u] = (c * (RTN_CT_CHUNK / 64u) + q) * 64u + lane;
 #pragma unroll
     for (int j = 0; j < 6; ++j) f.rec[u][j] = 0u;

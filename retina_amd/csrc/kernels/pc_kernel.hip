@@ -344,6 +344,18 @@ struct rtn_chunk {
   rtn_u64 my_pc, my_fwd, my_dlv;  // lane k holds group k's bitmap words until the chunk ends
 };
 
+// Record slot of the k-th forwarded frame of chunk c (RTN_REC_INDEX in retina_pc.h): a chunk's
+// records leave in blocks of RTN_REC_BLOCK = 64, and block j of chunk c sits at block slot
+// j * nchunks + c. The chunks' first blocks are then one dense stream, their second blocks the
+// next, and so on: at cfg2's 25 % forwarded the record stores fill two dense streams instead of
+// a quarter of every chunk-sized region (-4 % kernel time, in-process A/B on one box).
+__device__ __forceinline__ rtn_u64 rtn_nchunks(rtn_u32 n) {
+  return ((rtn_u64)n + 64u * RTN_CHUNK_GROUPS - 1u) / (64u * RTN_CHUNK_GROUPS);
+}
+__device__ __forceinline__ rtn_u64 rtn_rec_slot(rtn_u64 nch, rtn_u64 c, rtn_u32 k) {
+  return ((rtn_u64)(k >> 6) * nch + c) * 64u + (k & 63u);
+}
+
 
 // Records leave through a per-wave LDS ring of 256 records (6 KB) as whole 128-record blocks:
 // three full-width 16-B-per-lane stores per 3 KB, every line written whole.
@@ -360,9 +372,11 @@ __device__ __forceinline__ void rtn_flush(const rtn_args& a, const rtn_u64* ring
   if (a.flags & 4u) {
     // connection-stage entries (8 B) share the records' indices: same block, 128-B lines
     const rtn_u32 nc = ((nrecs + 1u) / 2u + 7u) & ~7u;
+    // (a 64-entry block is 32 lanes; a 128-record flush spans two blocks)
     const rtn_v4u* csrc = reinterpret_cast<const rtn_v4u*>(cring + (ch.nflushed & (RTN_RING - 1u)));
-    rtn_v4u* cdst = reinterpret_cast<rtn_v4u*>(a.conn + ch.rec_base + ch.nflushed);
-    if (lane < nc) RTN_ST(cdst + lane, csrc[lane]);
+    const rtn_u64 nch = rtn_nchunks(a.n);
+    rtn_v4u* cdst = reinterpret_cast<rtn_v4u*>(a.conn + rtn_rec_slot(nch, ch.rec_base / (64u * RTN_CHUNK_GROUPS), ch.nflushed));
+    if (lane < nc) RTN_ST(lane < 32u ? cdst + lane : cdst + nch * 32u + (lane - 32u), csrc[lane]);
   }
 #ifndef RTN_NO_PAD_TAIL
   // whole 128-B lines only: the block starts line-aligned and the tail is padded with stale ring
@@ -383,16 +397,25 @@ __device__ __forceinline__ void rtn_flush(const rtn_args& a, const rtn_u64* ring
   base = __shfl(base, 0);
   const rtn_u64 cap = (rtn_u64)((a.n + 511u) / 512u) * 512u - 1024u;
   rtn_v4u* dst = reinterpret_cast<rtn_v4u*>(a.recs + (((rtn_u64)base % cap) & ~15ull));
+#elif defined(RTN_EXP_REC_CHUNK)
+  // experiment: the earlier layout, records dense per chunk at chunk * 512 + k (timing only)
+  rtn_v4u* dst = reinterpret_cast<rtn_v4u*>(a.recs + ch.rec_base + ch.nflushed);
 #elif defined(RTN_EXP_REC_WRAP)
   // experiment: every chunk's records land in one of RTN_EXP_REC_WRAP regions (L2-resident)
   rtn_v4u* dst = reinterpret_cast<rtn_v4u*>(a.recs + (ch.rec_base / (64u * RTN_CHUNK_GROUPS) % RTN_EXP_REC_WRAP) * (64u * RTN_CHUNK_GROUPS) + ch.nflushed);
 #else
-  rtn_v4u* dst = reinterpret_cast<rtn_v4u*>(a.recs + ch.rec_base + ch.nflushed);
+  // a 64-record block is 96 lanes; a 128-record flush (RTN_FLUSH) spans two blocks
+  const rtn_u64 nch = rtn_nchunks(a.n);
+  rtn_v4u* dst = reinterpret_cast<rtn_v4u*>(a.recs + rtn_rec_slot(nch, ch.rec_base / (64u * RTN_CHUNK_GROUPS), ch.nflushed));
 #endif
 #pragma unroll
   for (rtn_u32 j = 0; j < 3u; ++j) {
     const rtn_u32 k = lane + 64u * j;
+#if defined(RTN_EXP_REC_STRIDE) || defined(RTN_EXP_REC_DENSE) || defined(RTN_EXP_REC_WRAP) || defined(RTN_EXP_REC_CHUNK)
     if (k < nv4) RTN_ST(dst + k, src[k]);
+#else
+    if (k < nv4) RTN_ST(k < 96u ? dst + k : dst + nch * 96u + (k - 96u), src[k]);
+#endif
   }
 }
 
@@ -518,7 +541,7 @@ __device__ __forceinline__ void rtn_group(const rtn_args& a, rtn_u32 g, rtn_u32 
       cring[r & (RTN_RING - 1u)] = (rtn_u64)h | ((rtn_u64)info << 32);
 #if RTN_CONN_WORDS > 0
 #pragma unroll
-      for (int j = 0; j < RTN_CONN_WORDS; ++j) a.conn_dlv[(ch.rec_base + r) * RTN_CONN_WORDS + j] = cm[j];
+      for (int j = 0; j < RTN_CONN_WORDS; ++j) a.conn_dlv[rtn_rec_slot(rtn_nchunks(a.n), ch.rec_base / (64u * RTN_CHUNK_GROUPS), r) * RTN_CONN_WORDS + j] = cm[j];
 #endif
     }
   }
@@ -857,7 +880,7 @@ extern "C" __global__ void __launch_bounds__(RTN_PD_THREADS) rtn_pd_kernel(rtn_p
     const rtn_u32 q = w * G + u;
     const rtn_u64 word = __shfl(wj, (int)q);
     has[u] = ch * 8u + q < nw && ((word >> lane) & 1ull);
-    r[u] = (rtn_u64)ch * 512u + pre[u] + (rtn_u32)__popcll(word & lane_lt);
+    r[u] = rtn_rec_slot(rtn_nchunks(a.n), ch, pre[u] + (rtn_u32)__popcll(word & lane_lt));
 #pragma unroll
     for (int j = 0; j < 6; ++j) rec[u][j] = 0u;
     slot[u] = 0xFFFFFFFFu;

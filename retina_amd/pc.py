@@ -302,7 +302,7 @@ class PCOutputs:
         pc = np.unpackbits(pc_bm.view(np.uint8), bitorder="little")[:n].astype(bool)
         fwd = np.unpackbits(fwd_bm.view(np.uint8), bitorder="little")[:n].astype(bool)
         recs_all = self.l4.cpu().numpy().view(L4_DTYPE)
-        idx = _segment_index(fwd_bm)
+        idx = _fwd_index(fwd_bm, n)
         recs = decode_l4(recs_all[idx], np.nonzero(fwd)[0])
         out = {"pc": pc, "fwd": fwd, "l4": recs}
         if self.addr6 is not None:
@@ -342,9 +342,29 @@ def _rank_index(frames: np.ndarray) -> np.ndarray:
 
 
 def _segment_index(bm: np.ndarray) -> np.ndarray:
-    """Record-array index of every set bit of `bm`, in frame order."""
+    """Index of every set bit of `bm` in a chunk-dense stream (addr6 / dlv_records), frame order."""
     bits = np.unpackbits(bm.view(np.uint8), bitorder="little").astype(np.int64)
     return _rank_index(np.nonzero(bits)[0])
+
+
+REC_BLOCK = 64  # RTN_REC_BLOCK (include/retina_pc.h)
+
+
+def _rec_index(frames: np.ndarray, n: int) -> np.ndarray:
+    """RTN_REC_INDEX of each forwarded frame (ascending frame indices): the l4 / conn / conn_dlv /
+    rtn_ct_entry_t / PacketDeliver-counts slot. Block k // 64 of chunk c sits at block slot
+    (k // 64) * nchunks + c."""
+    dense = _rank_index(frames)
+    chunk = dense // CHUNK_FRAMES
+    k = dense - chunk * CHUNK_FRAMES
+    nch = (n + CHUNK_FRAMES - 1) // CHUNK_FRAMES
+    return ((k // REC_BLOCK) * nch + chunk) * REC_BLOCK + k % REC_BLOCK
+
+
+def _fwd_index(bm: np.ndarray, n: int) -> np.ndarray:
+    """RTN_REC_INDEX of every set bit of the forwarded bitmap `bm`, in frame order."""
+    bits = np.unpackbits(bm.view(np.uint8), bitorder="little").astype(np.int64)
+    return _rec_index(np.nonzero(bits)[0], n)
 
 
 class PacketContinue:
@@ -445,7 +465,7 @@ def decode_pd(counts, bitmap, pc_out: PCOutputs, n_stmts: int) -> tuple[np.ndarr
     n = pc_out.n
     fwd_bm = pc_out.fwd_bitmap.cpu().numpy().view(np.uint64)
     fwd = np.nonzero(np.unpackbits(fwd_bm.view(np.uint8), bitorder="little")[:n])[0]
-    rec = _rank_index(fwd)
+    rec = _rec_index(fwd, n)
     bm = bitmap.cpu().numpy().view(np.uint64)
     hit = np.unpackbits(bm.view(np.uint8), bitorder="little")[:n].astype(bool)
     sel = hit[fwd]
@@ -554,7 +574,7 @@ def decode_ct(entries, pc_out: PCOutputs) -> np.ndarray:
     """rtn_ct_entry_t of the forwarded frames in frame order: (slot, status) uint32 pairs."""
     fwd_bm = pc_out.fwd_bitmap.cpu().numpy().view(np.uint64)
     e = entries.cpu().numpy().view(np.uint32).reshape(-1, 2)
-    return e[_segment_index(fwd_bm)]
+    return e[_fwd_index(fwd_bm, pc_out.n)]
 
 
 def split_slab(slab: np.ndarray, stride: int) -> tuple[np.ndarray, np.ndarray]:
