@@ -97,3 +97,31 @@ def test_headers_are_c(tmp_path):
                         "-L/opt/rocm/lib", "-Wl,-rpath,/opt/rocm/lib"], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
     assert len(names) > 40
+
+
+def test_rec_index_macro_matches_host_decoder(tmp_path):
+    """RTN_REC_INDEX (retina_pc.h) and pc._rec_index (the decoder the parity tests use) agree, and
+    the index is a bijection of every (chunk, rank) pair onto [0, ceil(n/512)*512)."""
+    import subprocess
+
+    import numpy as np
+
+    inc = Path(__file__).resolve().parent.parent / "include"
+    src = ('#include "retina_pc.h"\n#include <stdio.h>\n#include <inttypes.h>\n'
+           "int main(void) {\n  const uint32_t ns[] = {1u, 511u, 512u, 513u, 4097u, 33554432u};\n"
+           "  for (int i = 0; i < 6; ++i) for (uint32_t c = 0; c < 3; ++c) for (uint32_t k = 0; k < 512; k += 37)\n"
+           '    printf("%u %u %u %" PRIu64 "\\n", ns[i], c, k, RTN_REC_INDEX(ns[i], c, k));\n  return 0;\n}\n')
+    (tmp_path / "ri.c").write_text(src)
+    r = subprocess.run(["gcc", "-std=c11", "-Wall", "-Werror", f"-I{inc}", str(tmp_path / "ri.c"), "-o",
+                        str(tmp_path / "ri")], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    out = subprocess.run([str(tmp_path / "ri")], capture_output=True, text=True, check=True).stdout
+    for line in out.splitlines():
+        n, c, k, want = map(int, line.split())
+        frames = c * 512 + np.arange(k + 1)  # the chunk's first k+1 frames, all forwarded
+        assert pc._rec_index(frames, n)[-1] == want
+    for n in (1, 700, 5000):
+        nch = (n + 511) // 512
+        frames = np.arange(nch * 512)  # every slot of every chunk forwarded
+        idx = pc._rec_index(frames, n)
+        assert np.array_equal(np.sort(idx), np.arange(nch * 512))
