@@ -352,8 +352,13 @@ struct rtn_chunk {
 __device__ __forceinline__ rtn_u64 rtn_nchunks(rtn_u32 n) {
   return ((rtn_u64)n + 64u * RTN_CHUNK_GROUPS - 1u) / (64u * RTN_CHUNK_GROUPS);
 }
+#ifndef RTN_RB
+// RTN_REC_BLOCK. Other values are a timing-only switch (the table and PacketDeliver kernels read
+// 64-record blocks): 16 and 32 measured within 1 % of 64 on cfg2 (in-process A/B, one box).
+#define RTN_RB 64u
+#endif
 __device__ __forceinline__ rtn_u64 rtn_rec_slot(rtn_u64 nch, rtn_u64 c, rtn_u32 k) {
-  return ((rtn_u64)(k >> 6) * nch + c) * 64u + (k & 63u);
+  return ((rtn_u64)(k / RTN_RB) * nch + c) * RTN_RB + (k % RTN_RB);
 }
 
 
@@ -372,11 +377,11 @@ __device__ __forceinline__ void rtn_flush(const rtn_args& a, const rtn_u64* ring
   if (a.flags & 4u) {
     // connection-stage entries (8 B) share the records' indices: same block, 128-B lines
     const rtn_u32 nc = ((nrecs + 1u) / 2u + 7u) & ~7u;
-    // (a 64-entry block is 32 lanes; a 128-record flush spans two blocks)
+    // (a block of RTN_RB entries is RTN_RB / 2 lanes; a flush may span several blocks)
     const rtn_v4u* csrc = reinterpret_cast<const rtn_v4u*>(cring + (ch.nflushed & (RTN_RING - 1u)));
     const rtn_u64 nch = rtn_nchunks(a.n);
     rtn_v4u* cdst = reinterpret_cast<rtn_v4u*>(a.conn + rtn_rec_slot(nch, ch.rec_base / (64u * RTN_CHUNK_GROUPS), ch.nflushed));
-    if (lane < nc) RTN_ST(lane < 32u ? cdst + lane : cdst + nch * 32u + (lane - 32u), csrc[lane]);
+    if (lane < nc) RTN_ST(cdst + (lane / (RTN_RB / 2u)) * nch * (RTN_RB / 2u) + lane % (RTN_RB / 2u), csrc[lane]);
   }
 #ifndef RTN_NO_PAD_TAIL
   // whole 128-B lines only: the block starts line-aligned and the tail is padded with stale ring
@@ -404,7 +409,7 @@ __device__ __forceinline__ void rtn_flush(const rtn_args& a, const rtn_u64* ring
   // experiment: every chunk's records land in one of RTN_EXP_REC_WRAP regions (L2-resident)
   rtn_v4u* dst = reinterpret_cast<rtn_v4u*>(a.recs + (ch.rec_base / (64u * RTN_CHUNK_GROUPS) % RTN_EXP_REC_WRAP) * (64u * RTN_CHUNK_GROUPS) + ch.nflushed);
 #else
-  // a 64-record block is 96 lanes; a 128-record flush (RTN_FLUSH) spans two blocks
+  // a block of RTN_RB records is RTN_RB * 3 / 2 lanes; a flush (RTN_FLUSH) may span several
   const rtn_u64 nch = rtn_nchunks(a.n);
   rtn_v4u* dst = reinterpret_cast<rtn_v4u*>(a.recs + rtn_rec_slot(nch, ch.rec_base / (64u * RTN_CHUNK_GROUPS), ch.nflushed));
 #endif
@@ -414,7 +419,7 @@ __device__ __forceinline__ void rtn_flush(const rtn_args& a, const rtn_u64* ring
 #if defined(RTN_EXP_REC_STRIDE) || defined(RTN_EXP_REC_DENSE) || defined(RTN_EXP_REC_WRAP) || defined(RTN_EXP_REC_CHUNK)
     if (k < nv4) RTN_ST(dst + k, src[k]);
 #else
-    if (k < nv4) RTN_ST(k < 96u ? dst + k : dst + nch * 96u + (k - 96u), src[k]);
+    if (k < nv4) RTN_ST(dst + (k / (RTN_RB * 3u / 2u)) * nch * (RTN_RB * 3u / 2u) + k % (RTN_RB * 3u / 2u), src[k]);
 #endif
   }
 }
