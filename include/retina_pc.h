@@ -124,6 +124,7 @@ typedef struct rtn_batch {
 #define RTN_REC_INDEX(n, chunk, k)                                                             \
   (((uint64_t)((k) / RTN_REC_BLOCK) * (((uint64_t)(n) + RTN_CHUNK_FRAMES - 1u) / RTN_CHUNK_FRAMES) + \
     (uint64_t)(chunk)) * RTN_REC_BLOCK + (uint64_t)((k) % RTN_REC_BLOCK))
+/* l4, addr6 and conn must be 16-byte aligned (RTN_EINVAL otherwise). */
 typedef struct rtn_pc_out {
   uint64_t* pc_bitmap;   /* [ceil(n/64)]  Actions.data contains PacketContinue               */
   uint64_t* fwd_bitmap;  /* [ceil(n/64)]  ... and L4Context::new succeeded (goes to conntrack) */

@@ -468,6 +468,9 @@ int32_t rtn_pc_run(rtn_pc_t* pc, const rtn_batch_t* in, rtn_pc_out_t* out, void*
   if (in->ext && (reinterpret_cast<uintptr_t>(in->ext) & 15u) != 0)
     return fail(RTN_EINVAL, "ext must be 16-byte aligned");
   if (!out->pc_bitmap || !out->fwd_bitmap || !out->l4) return fail(RTN_EINVAL, "pc_bitmap/fwd_bitmap/l4 required");
+  // record arrays leave in 16-B-per-lane stores
+  for (const void* o : {(const void*)out->l4, (const void*)out->addr6, (const void*)out->conn})
+    if ((reinterpret_cast<uintptr_t>(o) & 15u) != 0) return fail(RTN_EINVAL, "l4/addr6/conn must be 16-byte aligned");
   const uint32_t dw = pc->program->prog.deliver_words();
   if (dw > 0 && (!out->dlv_bitmap || !out->dlv_records))
     return fail(RTN_EINVAL, "program has packet-level callbacks: dlv_bitmap/dlv_records required");
