@@ -145,3 +145,26 @@ def test_large_tree_uses_nested_form_and_matches(gpu):
                                           payload=bytes(int(rng.integers(0, 5)))))
     slab, dlen = pc.pack_frames(frames, 128)
     helpers.assert_same(helpers.gpu_run(spec, slab, 128, dlen), helpers.oracle_run(spec, slab, 128, dlen), "large tree")
+
+
+def test_misaligned_record_array_is_einval(gpu):
+    """l4 / addr6 / conn take 16-B-per-lane stores: a misaligned array is refused (RTN_EINVAL)
+    before anything is launched, and the same context still runs on aligned outputs."""
+    import dataclasses
+
+    import torch
+
+    slab, dlen = synth.cfg2(1024, start=5)
+    ctx = pc.PacketContinue(pc.Program.from_spec(SETS["cfg2"]), 0)
+    d_slab = torch.from_numpy(slab).cuda()
+    d_dlen = torch.from_numpy(dlen.view(np.int16)).cuda()
+    out = ctx.alloc_outputs(len(dlen), conn=True)
+    for field in ("l4", "addr6", "conn"):
+        t = getattr(out, field)
+        bad = dataclasses.replace(out, **{field: torch.empty(t.numel() + 16, dtype=torch.uint8, device="cuda")[8:]})
+        with pytest.raises(pc.RetinaError) as e:
+            ctx.run(d_slab, 64, d_dlen, len(dlen), bad)
+        assert e.value.code == -22 and "16-byte aligned" in str(e.value)
+    ctx.run(d_slab, 64, d_dlen, len(dlen), out)
+    torch.cuda.synchronize()
+    assert int(out.counters.view(torch.int32)[1]) > 0
