@@ -51,6 +51,12 @@ typedef unsigned int rtn_v4u __attribute__((ext_vector_type(4)));
 #else
 #define RTN_ST(p, v) __builtin_nontemporal_store((v), (p))
 #endif
+// 8-B stores (bitmap words, delivery records, first-packet statement masks)
+#ifdef RTN_NT_SMALL
+#define RTN_ST8(p, v) __builtin_nontemporal_store((v), (p))
+#else
+#define RTN_ST8(p, v) (*(p) = (v))
+#endif
 #ifdef RTN_NT_LOADS
 #define RTN_LD(p) __builtin_nontemporal_load(p)
 #else
@@ -550,7 +556,7 @@ __device__ __forceinline__ void rtn_group(const rtn_args& a, rtn_u32 g, rtn_u32 
       cring[r & (RTN_RING - 1u)] = (rtn_u64)h | ((rtn_u64)info << 32);
 #if RTN_CONN_WORDS > 0
 #pragma unroll
-      for (int j = 0; j < RTN_CONN_WORDS; ++j) a.conn_dlv[rtn_rec_slot(rtn_nchunks(a.n), ch.rec_base / (64u * RTN_CHUNK_GROUPS), r) * RTN_CONN_WORDS + j] = cm[j];
+      for (int j = 0; j < RTN_CONN_WORDS; ++j) RTN_ST8(a.conn_dlv + rtn_rec_slot(rtn_nchunks(a.n), ch.rec_base / (64u * RTN_CHUNK_GROUPS), r) * RTN_CONN_WORDS + j, cm[j]);
 #endif
     }
   }
@@ -605,9 +611,9 @@ __device__ __forceinline__ void rtn_group(const rtn_args& a, rtn_u32 g, rtn_u32 
 #endif
       const rtn_u64 slot_i = ch.rec_base + ch.ndlv + (rtn_u32)__popcll(dlvm & lane_lt);
       rtn_u64* dp = a.dlv_recs + slot_i * (1u + RTN_DELIVER_WORDS);
-      dp[0] = (rtn_u64)i;
+      RTN_ST8(dp, (rtn_u64)i);
 #pragma unroll
-      for (int j = 0; j < RTN_DELIVER_WORDS; ++j) dp[1 + j] = dm[j];
+      for (int j = 0; j < RTN_DELIVER_WORDS; ++j) RTN_ST8(dp + 1 + j, dm[j]);
     }
     ch.ndlv += (rtn_u32)__popcll(dlvm);
   }
@@ -747,10 +753,10 @@ __device__ __forceinline__ void rtn_run(const rtn_args& a) {
     rtn_wave_sync();
 #endif
     if (lane < ge - gb) {
-      a.pc_bm[gb + lane] = ch.my_pc;
-      a.fwd_bm[gb + lane] = ch.my_fwd;
+      RTN_ST8(a.pc_bm + gb + lane, ch.my_pc);
+      RTN_ST8(a.fwd_bm + gb + lane, ch.my_fwd);
 #if RTN_DELIVER_WORDS > 0
-      a.dlv_bm[gb + lane] = ch.my_dlv;
+      RTN_ST8(a.dlv_bm + gb + lane, ch.my_dlv);
 #endif
     }
   }
