@@ -985,7 +985,15 @@ extern "C" __global__ void __launch_bounds__(RTN_PD_THREADS) rtn_pd_kernel(rtn_p
     if (lane == 0u && ch * 8u + q < nw) a.pd_bm[ch * 8u + q] = mb;
     if (dl) {
 #pragma unroll
-      for (int j = 0; j < RTN_PD_S; ++j) a.counts[r[u] * RTN_PD_S + j] = cnt[j];
+      for (int j = 0; j < RTN_PD_S; ++j) {
+#ifndef RTN_PD_TEMPORAL
+        // written once, read by the host or a later launch: non-temporal (cfg2 PacketDeliver
+        // 0.4387 -> 0.4177 ms, in-process A/B on one box)
+        __builtin_nontemporal_store(cnt[j], a.counts + r[u] * RTN_PD_S + j);
+#else
+        a.counts[r[u] * RTN_PD_S + j] = cnt[j];
+#endif
+      }
     }
   }
 }
