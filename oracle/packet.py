@@ -184,9 +184,14 @@ def payload_ok(d: bytes, dl: int) -> bool:
     return c is not None and c.offset < dl and c.offset + c.length <= dl
 
 
-def evaluate(tree: PacketTree, frame: bytes, dl: int | None = None):
+def evaluate(tree: PacketTree, frame: bytes, dl: int | None = None, chains: bool = True,
+             trace: dict | None = None):
     """Run the generated packet_continue for `tree` on one frame.
-    Returns (actions_data, [deliver statement index, ...] in call order)."""
+    Returns (actions_data, [deliver statement index, ...] in call order).
+
+    chains=False runs every sibling whose condition holds, as if no `else if` had been emitted
+    (test instrument: the tree's content without filtergen's chaining). `trace`, if given, counts
+    in trace["skipped"] the siblings an `else if` chain skipped although their condition held."""
     d = bytes(frame)
     dl = len(d) if dl is None else dl
     d = d + bytes(max(0, 256 - len(d)))
@@ -221,9 +226,13 @@ def evaluate(tree: PacketTree, frame: bytes, dl: int | None = None):
                 cont = c.if_else
             if not cont:
                 chain_taken = False
-            go = run and not chain_taken
+            go = run and (not chain_taken or not chains)
             matched = False
             env2 = env
+            if trace is not None and run and chain_taken and chains:
+                hit = (parse(d, dl, c.pred.proto, env[node.pred.proto]) is not None) if c.pred.unary \
+                    else eval_binary(d, env[c.pred.proto], c.pred)
+                trace["skipped"] = trace.get("skipped", 0) + int(hit)
             if go:
                 if c.pred.unary:
                     h = parse(d, dl, c.pred.proto, env[node.pred.proto])

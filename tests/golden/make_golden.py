@@ -82,6 +82,15 @@ def python_crosscheck(spec: str, slab: np.ndarray, dlen: np.ndarray, res: dict, 
         assert dm == got, (spec, i, fired)
         ctx = packet.l4context(fr, dl) if act & 1 else None
         assert (ctx is not None) == bool(res["fwd"][i]), (spec, i)
+        if ctx is not None:
+            # every L4Context field, addresses included (pdu.rs:66-84)
+            x = res["l4"][i]
+            w = 4 if ctx.ver == 4 else 16
+            assert (int(x["ver"]), int(x["proto"]), int(x["sport"]), int(x["dport"]), int(x["offset"]),
+                    int(x["length"]), int(x["seq"]), int(x["ack"]), int(x["flags"]), bytes(x["src"]),
+                    bytes(x["dst"])) == (ctx.ver, ctx.proto, ctx.sport, ctx.dport, ctx.offset, ctx.length, ctx.seq,
+                                         ctx.ack, ctx.flags, ctx.src.to_bytes(w, "big") + bytes(16 - w),
+                                         ctx.dst.to_bytes(w, "big") + bytes(16 - w)), (spec, i)
 
 
 def conn_expected(spec: str, slab: np.ndarray, dlen: np.ndarray, fwd: np.ndarray) -> tuple[np.ndarray, np.ndarray]:

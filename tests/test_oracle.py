@@ -160,3 +160,48 @@ def test_hw_filter_string_matches_oracle(fset):
     assert hw == filterlang.PacketTree(filterlang.load_spec(SETS[fset])).to_filter_string()
     if hw:
         filterlang.parse_filter(hw)
+
+
+def _l4_corpora():
+    import corpus as C
+
+    t = np.load(GOLD / "traces.npz")
+    a = np.load(GOLD / "corpus_adversarial.npz")
+    r, rd = pc.pack_frames(C.random_frames(4000, seed=77), 128)
+    s3, d3 = synth.cfg3(3000, start=4242)
+    s4, d4 = synth.cfg4(3000, start=4343)
+    s2, d2 = synth.cfg2(1000, start=99)
+    s2 = np.pad(s2.reshape(-1, 64), ((0, 0), (0, 64))).reshape(-1)
+    return {"traces": (t["slab"], t["dlen"]), "adversarial": (a["slab"], a["dlen"]), "random": (r, rd),
+            "synth": (np.concatenate([s2, s3, s4]), np.concatenate([d2, d3, d4]))}
+
+
+@pytest.mark.parametrize("name", ["traces", "adversarial", "random", "synth"])
+def test_python_l4context_every_field_vs_c_oracle(name):
+    """The two restatements of L4Context::new (pdu.rs:86-171) -- oracle/packet.py (pure Python)
+    and the generated C (oracle/cgen.py) -- agree on every field of every frame: existence,
+    IP version, both addresses (all 16 bytes for IPv6), ports, protocol, offset, length, seq, ack
+    and flags. Under the match-all set every frame is accepted, so the C oracle builds the
+    L4Context of every frame that has one."""
+    slab, dlen = _l4_corpora()[name]
+    r = helpers.oracle_run(SETS["match_all"], slab, 128, dlen)
+    assert r["pc"].all()
+    recs = {int(x["idx"]): x for x in r["rec"]}
+    b = slab.reshape(-1, 128)
+    n_v6 = 0
+    for i in range(len(dlen)):
+        c = packet.l4context(b[i].tobytes() + bytes(128), int(dlen[i]))
+        assert (c is not None) == bool(r["fwd"][i]) == (i in recs), (name, i)
+        if c is None:
+            continue
+        x = recs[i]
+        w = 4 if c.ver == 4 else 16
+        src = c.src.to_bytes(w, "big") + bytes(16 - w)
+        dst = c.dst.to_bytes(w, "big") + bytes(16 - w)
+        got = (int(x["ver"]), int(x["proto"]), int(x["sport"]), int(x["dport"]), int(x["offset"]), int(x["length"]),
+               int(x["seq"]), int(x["ack"]), int(x["flags"]), bytes(x["src"]), bytes(x["dst"]))
+        assert got == (c.ver, c.proto, c.sport, c.dport, c.offset, c.length, c.seq, c.ack, c.flags, src, dst), (name, i)
+        n_v6 += c.ver == 6
+    assert len(recs) > 0
+    if name in ("adversarial", "random", "synth"):
+        assert n_v6 > 0
