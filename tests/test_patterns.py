@@ -179,3 +179,15 @@ def test_cfg_sets_match_on_golden_with_helpers():
     r = helpers.oracle_run(SETS["cfg4"], slab, 128, dlen)
     epc, _ = patterns.evaluate_batch(patterns.PatternSet(subs), slab, 128, dlen)
     assert np.array_equal(r["pc"], np.array(epc))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(12))
+def test_gpu_random_sets(gpu, seed):
+    """The product (compiler + gfx950 kernel) on random subscription sets: bit-exact against the
+    tree-based C oracle on the adversarial + synthetic corpus (the CPU test above ties that
+    oracle to pattern semantics), in 128-B monolithic slots and in the split layout."""
+    spec = randsubs.to_toml(randsubs.random_subs(1000 + seed))
+    slab, dlen = _random_corpus()
+    exp = helpers.oracle_run(spec, slab, 128, dlen)
+    helpers.assert_same(helpers.gpu_run(spec, slab, 128, dlen, split=bool(seed & 1)), exp, f"random set {seed}")
