@@ -125,7 +125,7 @@ def load_traffic(cfg: str, n: int):
 
 
 def e2e_rate(ctx, slab: np.ndarray, dlen: np.ndarray, stride: int, dev, chunk: int = 1 << 21,
-             nstreams: int = 4) -> dict:
+             nstreams: int = 4, dl_le64: bool = False) -> dict:
     """End-to-end rate from pinned host memory: H2D of the header slab + data_len, the kernel,
     D2H of the bitmaps and L4Context records, pipelined over chunks on `nstreams` streams."""
     import torch
@@ -149,7 +149,7 @@ def e2e_rate(ctx, slab: np.ndarray, dlen: np.ndarray, stride: int, dev, chunk: i
             with torch.cuda.stream(st):
                 d_slab[:m * stride].copy_(h_slab[s * stride:(s + m) * stride], non_blocking=True)
                 d_dlen[:m].copy_(h_dlen[s:s + m], non_blocking=True)
-                ctx.run(d_slab, stride, d_dlen, m, out, stream=st)
+                ctx.run(d_slab, stride, d_dlen, m, out, stream=st, dl_le64=dl_le64)
                 h_out[k % nstreams].copy_(out.l4, non_blocking=True)
                 nb = out.pc_bitmap.numel()
                 h_bm[k % nstreams][:nb].copy_(out.pc_bitmap, non_blocking=True)
@@ -189,7 +189,7 @@ callback = "t2_cb"
 """
 
 
-def pd_rate(cfg, d_slab, stride, d_dlen, n, d_ext, device, stream, steps) -> dict:
+def pd_rate(cfg, d_slab, stride, d_dlen, n, d_ext, device, stream, steps, dl_le64) -> dict:
     """Side measurement: rtn_pd_run over the batch with every frame's connection established
     before the batch and holding PacketDeliver (the worst case: every forwarded frame evaluates
     the tree and gathers its connection's state)."""
@@ -200,7 +200,7 @@ def pd_rate(cfg, d_slab, stride, d_dlen, n, d_ext, device, stream, steps) -> dic
     prog = pc.Program.from_spec(PD_SPEC)
     ctx = pc.PacketContinue(prog, device)
     out = ctx.alloc_outputs(n, addr6=True, counters=False, conn=True)
-    ctx.run(d_slab, stride, d_dlen, n, out, stream=stream, ext=d_ext)
+    ctx.run(d_slab, stride, d_dlen, n, out, stream=stream, ext=d_ext, dl_le64=dl_le64)
     ct = pc.ConnTable(device, 26, 1 << 26)
     ent = ct.process(out, stream=stream)
     ct.process(out, out=ent, stream=stream)  # every opener now predates the batch
@@ -290,6 +290,9 @@ def main() -> None:
         d_slab = torch.from_numpy(slab).to(dev)
         run_stride = stride
     d_dlen = torch.from_numpy(dlen.view(np.int16)).to(dev)
+    # 64-byte slots without ext: assert (RTN_BATCH_DL_LE64) what the generator guarantees, after
+    # checking it on the host
+    dl_le64 = run_stride == 64 and d_ext is None and int(dlen.max(initial=0)) <= 64
 
     prog = pc.Program.from_spec(spec_for(cfg))
     ctx = pc.PacketContinue(prog, local)
@@ -297,7 +300,7 @@ def main() -> None:
     stream = torch.cuda.current_stream(dev)
 
     for _ in range(args.warmup):
-        ctx.run(d_slab, run_stride, d_dlen, n, out, stream=stream, ext=d_ext)
+        ctx.run(d_slab, run_stride, d_dlen, n, out, stream=stream, ext=d_ext, dl_le64=dl_le64)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -307,7 +310,7 @@ def main() -> None:
     t0 = time.perf_counter()
     ev0.record(stream)
     for _ in range(args.steps):
-        ctx.run(d_slab, run_stride, d_dlen, n, out, stream=stream, ext=d_ext)
+        ctx.run(d_slab, run_stride, d_dlen, n, out, stream=stream, ext=d_ext, dl_le64=dl_le64)
     ev1.record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -322,12 +325,12 @@ def main() -> None:
     if not args.no_conn and world == 1:
         cout = ctx.alloc_outputs(n, addr6=True, counters=False, conn=True)
         for _ in range(3):
-            ctx.run(d_slab, run_stride, d_dlen, n, cout, stream=stream, ext=d_ext)
+            ctx.run(d_slab, run_stride, d_dlen, n, cout, stream=stream, ext=d_ext, dl_le64=dl_le64)
         c0 = torch.cuda.Event(enable_timing=True)
         c1 = torch.cuda.Event(enable_timing=True)
         c0.record(stream)
         for _ in range(args.steps):
-            ctx.run(d_slab, run_stride, d_dlen, n, cout, stream=stream, ext=d_ext)
+            ctx.run(d_slab, run_stride, d_dlen, n, cout, stream=stream, ext=d_ext, dl_le64=dl_le64)
         c1.record(stream)
         torch.cuda.synchronize(dev)
         cms = c0.elapsed_time(c1) / args.steps
@@ -351,7 +354,7 @@ def main() -> None:
         ctms = k0.elapsed_time(k1) / args.steps
         ct_stats = ct.stats()
         del ct
-        pd_stage = pd_rate(cfg, d_slab, run_stride, d_dlen, n, d_ext, local, stream, args.steps) \
+        pd_stage = pd_rate(cfg, d_slab, run_stride, d_dlen, n, d_ext, local, stream, args.steps, dl_le64) \
             if cfg == "cfg2" else None
         conn_stage = {"kernel_ms": round(cms, 4), "mpps": round(n / cms / 1e3, 1),
                       "vs_filter_only": round(kern_ms / cms, 3),
@@ -383,7 +386,7 @@ def main() -> None:
             cpu = cpu_baseline(cfg, slab, dlen, stride)
         e2e = None
         if not args.no_e2e and world == 1:
-            e2e = e2e_rate(ctx, slab, dlen, stride, dev)
+            e2e = e2e_rate(ctx, slab, dlen, stride, dev, dl_le64=dl_le64)
         line = {
             "metric": METRIC,
             "value": round(value, 1),

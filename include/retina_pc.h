@@ -92,6 +92,16 @@ typedef struct rtn_conn {
 #define RTN_CONN_IPV6(i) (((i) >> 29) & 1u) /* the record is IPv6 (its addresses are in addr6)  */
 #define RTN_CONN_UDP(i) (((i) >> 30) & 1u)  /* L4Context.proto is UDP (else TCP)              */
 
+/* Largest batch rtn_pc_run accepts (frame indices stay 32-bit inside the kernels). */
+#define RTN_MAX_FRAMES (1u << 31)
+
+/* rtn_batch_t.flags */
+#define RTN_BATCH_DL_LE64 1u /* the caller asserts data_len[i] <= 64 for every frame (see below)  */
+
+/* Status bits (counters[3], rtn_pc_take_status): frames whose results are not the reference's. */
+#define RTN_STATUS_HDR_PAST_SLOT 1u /* 64-B slots, no ext: an IP frame's headers run past byte 64 */
+#define RTN_STATUS_DL_PAST_SLOT 2u  /* RTN_BATCH_DL_LE64 asserted, but a frame has data_len > 64  */
+
 /* A batch of frames laid out for coalesced HBM reads, in one of two layouts:
  *  - monolithic (ext == NULL): slot i (stride bytes, a multiple of 64) holds the first
  *    min(data_len[i], stride) bytes of frame i;
@@ -99,14 +109,22 @@ typedef struct rtn_conn {
  *    (64 bytes) bytes [64, 128). The kernel reads ext[i] only for frames whose headers run past
  *    byte 64 (IPv6, IPv4 options, VLAN + options), so a frame costs 64 B of HBM reads unless it
  *    needs more -- a 128-byte monolithic slot costs a whole 128-B line for every frame.
- * A frame whose headers do not fit (stride 64 without ext) raises counters[3] bit 0. */
+ * 64-byte slots without ext hold every header only when no frame's headers pass byte 64. The
+ * caller must make that checkable: either every data_len is <= 64 and flags has
+ * RTN_BATCH_DL_LE64 (a frame cannot be parsed past its data_len, so the slot holds everything
+ * the parse reads), or counters is passed so that the status word reaches the caller. Otherwise
+ * rtn_pc_run refuses the batch (RTN_EINVAL). A frame that breaks the layout is reported in
+ * counters[3] (RTN_STATUS_*) and, when counters is NULL, in the context's sticky status word
+ * (rtn_pc_take_status). */
 typedef struct rtn_batch {
   const uint8_t* slab;
   uint64_t stride;
   const uint16_t* data_len; /* Mbuf::data_len of each frame (mbuf.rs:95-97) */
-  uint32_t n;
+  uint32_t n;               /* <= RTN_MAX_FRAMES                                          */
   uint32_t core_id;         /* the calling lcore (passed to CoreId callbacks by the host) */
   const uint8_t* ext;       /* split layout: bytes [64, 128) of each frame, 64-byte slots */
+  uint32_t flags;           /* RTN_BATCH_*                                                */
+  uint32_t reserved;        /* 0                                                          */
 } rtn_batch_t;
 
 /* Records are ranked per chunk of RTN_CHUNK_FRAMES frames, in frame order: the k-th forwarded
@@ -132,14 +150,27 @@ typedef struct rtn_pc_out {
   uint8_t* addr6;        /* optional [ceil(n/512)*512][32]: src|dst of the IPv6 records   */
   uint64_t* dlv_bitmap;  /* [ceil(n/64)] frames with >= 1 packet-level callback (if any)     */
   uint64_t* dlv_records; /* [ceil(n/512)*512][1 + deliver_words]: frame index, statement mask */
-  uint32_t* counters;    /* optional [8] (32 B, 8-B aligned): pc, fwd, dlv totals, status bits, then
-                          u64 data_len sum of all frames (TOTAL_BYTE) and u64 data_len sum of the
-                          frames not accepted (IGNORED_BY_PACKET_FILTER_BYTE, rx_core.rs:129-141);
-                          zeroed per run (NULL: no totals, no memset -- one kernel launch) */
+  uint32_t* counters;    /* optional [16] (RTN_COUNTERS_BYTES = 64 B, 8-B aligned), zeroed per run
+                          (NULL: no totals, no memset -- one kernel launch); RTN_CNT_* below */
   rtn_conn_t* conn;      /* optional [ceil(n/512)*512]: connection stage, indexed like l4       */
   uint64_t* conn_dlv;    /* [ceil(n/512)*512][conn_words] first-packet statement masks; required
                           with conn when the program has first-packet statements           */
 } rtn_pc_out_t;
+
+/* The counters block (u32 word offsets; the byte sums are u64 over two words). The stats names
+ * are the reference's thread-local counters (core/src/stats/mod.rs:9-27) as rx_core.rs:127-139
+ * and Subscription::process_packet (subscription/mod.rs:102-111) update them per frame. */
+#define RTN_COUNTERS_BYTES 64u
+#define RTN_CNT_PC 0u          /* u32: Actions.data has PacketContinue (TOTAL_PKT - IGNORED_BY_PACKET_FILTER_PKT) */
+#define RTN_CNT_FWD 1u         /* u32: ... and L4Context::new Ok (frames handed to conntrack)  */
+#define RTN_CNT_DLV 2u         /* u32: frames with >= 1 packet-level callback                  */
+#define RTN_CNT_STATUS 3u      /* u32: RTN_STATUS_* bits                                       */
+#define RTN_CNT_TOTAL_BYTE 4u  /* u64: TOTAL_BYTE (data_len of every frame)                    */
+#define RTN_CNT_IGNORED_BYTE 6u /* u64: IGNORED_BY_PACKET_FILTER_BYTE                          */
+#define RTN_CNT_TCP_PKT 8u     /* u32: TCP_PKT (forwarded, L4Context.proto == 6)               */
+#define RTN_CNT_UDP_PKT 9u     /* u32: UDP_PKT (forwarded, proto 17)                           */
+#define RTN_CNT_TCP_BYTE 10u   /* u64: TCP_BYTE                                                */
+#define RTN_CNT_UDP_BYTE 12u   /* u64: UDP_BYTE                                                */
 
 typedef struct rtn_program_info {
   uint32_t n_subscriptions;
@@ -200,6 +231,9 @@ int32_t rtn_pc_create(const char* spec, size_t len, int device, rtn_pc_t** out);
 int32_t rtn_pc_create_from_program(rtn_program_t* p, int device, rtn_pc_t** out);
 /* Launch on `stream` (a hipStream_t, NULL = default). Asynchronous. */
 int32_t rtn_pc_run(rtn_pc_t* pc, const rtn_batch_t* in, rtn_pc_out_t* out, void* stream);
+/* RTN_STATUS_* bits raised by runs without counters since the last call, then cleared.
+ * Synchronizes the device. */
+int32_t rtn_pc_take_status(rtn_pc_t* pc, uint32_t* status);
 /* Workgroups per launch (0 = default). */
 int32_t rtn_pc_set_grid(rtn_pc_t* pc, uint32_t blocks);
 int32_t rtn_pc_destroy(rtn_pc_t* pc);

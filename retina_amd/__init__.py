@@ -4,6 +4,6 @@ The product is the HIP kernel generated per subscription set by the C++ filter c
 through the C ABI in include/retina_pc.h (libretina_pc.so). `pc` is the ctypes binding,
 `subscription` the host-side mirror of Retina's Subscription/filter API for this stage.
 """
-from . import pc  # noqa: F401
+from . import pc, subscription  # noqa: F401
 
-__all__ = ["pc"]
+__all__ = ["pc", "subscription"]

@@ -31,48 +31,21 @@ typedef unsigned int rtn_v4u __attribute__((ext_vector_type(4)));
 #define RTN_DELIVER_WORDS 0
 #endif
 #define RTN_DM_WORDS (RTN_DELIVER_WORDS > 0 ? RTN_DELIVER_WORDS : 1)
-#ifndef RTN_CHUNK_GROUPS
 // groups per output chunk: 512 frames (RTN_CHUNK_FRAMES in retina_pc.h). A chunk is one wave's
 // unit of work; at 2^25 frames 8 groups measured 6-9 % faster than 16 (the last chunks finish
 // sooner) and 2-3 % faster than 4 (fewer partial record blocks).
 #define RTN_CHUNK_GROUPS 8u
-#endif
-#ifndef RTN_UNROLL
-#define RTN_UNROLL 1  // groups per loop iteration per wave (2 measured no faster, 12 more VGPRs)
-#endif
 // Record-block stores (records, rtn_conn_t, IPv6 addresses) are non-temporal: each line is
-// written once and read by a later launch, so it streams past the caches. Measured against plain
+// written once and read by a later launch, so it streams past the caches (measured against plain
 // stores, in-process on one box, with the interleaved record layout: cfg2 -1.1 %, cfg3 -14.5 %,
-// cfg4 -10.4 % (RTN_TEMPORAL_STORES keeps plain stores as a switch).
-#if defined(RTN_SC1_STORES)
-#define RTN_ST(p, v) asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory")
-#elif defined(RTN_TEMPORAL_STORES)
-#define RTN_ST(p, v) (*(p) = (v))
-#else
+// cfg4 -10.4 %). The 8-B stores (bitmap words, delivery records) stay plain: the two half-line
+// bitmap stores of a block merge in L2.
 #define RTN_ST(p, v) __builtin_nontemporal_store((v), (p))
-#endif
-// 8-B stores (bitmap words, delivery records, first-packet statement masks)
-#ifdef RTN_NT_SMALL
-#define RTN_ST8(p, v) __builtin_nontemporal_store((v), (p))
-#else
 #define RTN_ST8(p, v) (*(p) = (v))
-#endif
-#ifdef RTN_NT_LOADS
-#define RTN_LD(p) __builtin_nontemporal_load(p)
-#else
-#define RTN_LD(p) (*(p))
-#endif
-// 64-byte slots load coalesced + LDS transpose (RTN_XPOSE) with non-temporal loads: every line
-// is touched once, so streaming it past the caches costs nothing (per-lane loads touch each
-// line four times and must not be non-temporal).
-#ifndef RTN_NO_XPOSE
-#define RTN_XPOSE 1
-#endif
-#ifdef RTN_XPOSE_TEMPORAL
-#define RTN_LD_STREAM(p) (*(p))
-#else
+// 64-byte slots load coalesced + LDS transpose with non-temporal loads: every line is touched
+// once, so streaming it past the caches costs nothing (per-lane loads of wider slots touch each
+// line four times and stay plain).
 #define RTN_LD_STREAM(p) __builtin_nontemporal_load(p)
-#endif
 
 struct rtn_l4rec {       // 24 B, the compacted L4Context of a forwarded packet (rtn_l4ctx_t)
   rtn_u32 src_ip4;       // u32::from(Ipv4Addr) (0 for IPv6; addresses in addr6 side array)
@@ -88,14 +61,15 @@ struct rtn_args {
   rtn_u64 stride;
   const unsigned short* dlen;
   rtn_u32 n;
-  rtn_u32 flags;              // bit0: write addr6 side array, bit1: accumulate counters
+  rtn_u32 flags;              // bit0: addr6, bit1: counters, bit2: conn, bit3: caller asserts data_len <= 64
   rtn_u64* pc_bm;             // [ceil(n/64)]  PacketContinue bit
   rtn_u64* fwd_bm;            // [ceil(n/64)]  PacketContinue && L4Context::new Ok
   rtn_l4rec* recs;            // [ceil(n/512)*512], dense per chunk
   unsigned char* addr6;       // [ceil(n/64)*64][32] (src, dst) raw bytes, IPv6 records only
   rtn_u64* dlv_bm;            // [ceil(n/64)]  any packet-level delivery
   rtn_u64* dlv_recs;          // [ceil(n/64)*64][1 + RTN_DELIVER_WORDS]  (pkt_idx, statement mask words)
-  rtn_u32* counters;          // [0] pc, [1] fwd, [2] dlv, [3] status bits, [4..5] bytes, [6..7] ignored bytes
+  rtn_u32* counters;          // [0] pc, [1] fwd, [2] dlv, [3] status, [4..5] bytes, [6..7] ignored bytes,
+                              // [8] tcp, [9] udp (forwarded), [10..11] tcp bytes, [12..13] udp bytes
   const unsigned char* ext;   // split layout: bytes 64..127 of each frame (64-byte slots), or null
   rtn_u64* conn;              // optional [ceil(n/512)*512] rtn_conn_t, indexed like recs (flags bit2)
   rtn_u64* conn_dlv;          // [ceil(n/512)*512][RTN_CONN_WORDS] first-packet statement masks
@@ -256,7 +230,6 @@ __device__ __forceinline__ void rtn_parse(const rtn_u32 (&w)[NW], rtn_u32 dl, rt
   const rtn_u32 src = ipm ? (rtn_u32)__builtin_ctzll(ipm) : 0u;
   const rtn_u32 ukey = __builtin_amdgcn_readlane(key, src);
   const bool uni = __ballot(ip && key != ukey) == 0ull;
-#ifndef RTN_NO_UNIFORM
   if (uni && ukey == (14u | (34u << 8))) {
     rtn_extract_c<NW, 14, 34>(w, v);         // Eth / IPv4 (IHL 5)
   } else if (uni && ukey == (18u | (38u << 8))) {
@@ -265,9 +238,7 @@ __device__ __forceinline__ void rtn_parse(const rtn_u32 (&w)[NW], rtn_u32 dl, rt
     rtn_extract_c<NW, 14, 54>(w, v);         // Eth / IPv6
   } else if (uni && ukey == (18u | (58u << 8))) {
     rtn_extract_c<NW, 18, 58>(w, v);         // Eth / 802.1Q / IPv6
-  } else
-#endif
-  {
+  } else {
     rtn_extract_v<NW>(w, q, v.l4off, v);
   }
   // L4Context::new (pdu.rs:86-171): payload = ip length - headers, checked_sub
@@ -281,8 +252,9 @@ __device__ __forceinline__ void rtn_parse(const rtn_u32 (&w)[NW], rtn_u32 dl, rt
 }
 
 struct rtn_acc {
-  rtn_u32 pc, fwd, dlv, status;
+  rtn_u32 pc, fwd, dlv, status, tcp;
   rtn_u64 bytes, ignored;  // this lane's data_len sums: all frames / frames not accepted (rx_core.rs:129-141)
+  rtn_u64 tcpb, udpb;      // ... forwarded TCP / UDP frames (process_packet, subscription/mod.rs:102-111)
 };
 
 // First 64 B of slot i. Lanes past n re-read the last slot (no branch, no zero fill); their
@@ -293,17 +265,17 @@ __device__ __forceinline__ void rtn_load_lo(const rtn_args& a, rtn_u32 i, rtn_u3
   const rtn_v4u* slot = reinterpret_cast<const rtn_v4u*>(a.slab + (rtn_u64)ic * a.stride);
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    const rtn_v4u x = RTN_LD(slot + k);
+    const rtn_v4u x = slot[k];
     w[4 * k + 0] = x.x; w[4 * k + 1] = x.y; w[4 * k + 2] = x.z; w[4 * k + 3] = x.w;
   }
   const rtn_u32 d = a.dlen[ic];
   dl = valid ? d : 0u;
 }
 
-#ifdef RTN_XPOSE
 // 64-byte slots, coalesced: the group's 4 KB arrive as four full-width 16-B-per-lane loads
-// (lane l of load k holds quarter l%4 of slot 16k + l/4) and an LDS tile (80-B pitch, conflict-
-// free ds_read_b128) turns them back into one slot per lane.
+// (lane l of load k holds quarter l%4 of slot 16k + l/4) and an LDS tile (one 64-B row per slot,
+// 16-B quarters XOR-swizzled by (row >> 2) & 3: conflict-free ds_write_b128 / ds_read_b128)
+// turns them back into one slot per lane.
 #define RTN_XPITCH 16u  // one 64-B slot per row, 16-B chunks XOR-swizzled by (row >> 2) & 3
 __device__ __forceinline__ void rtn_load_group(const rtn_args& a, rtn_u32 g, rtn_u32 lane, rtn_v4u (&q)[4], rtn_u32& dl) {
 #pragma unroll
@@ -329,7 +301,6 @@ __device__ __forceinline__ void rtn_xpose(rtn_u32* tile, rtn_u32 lane, const rtn
     w[4 * j + 0] = x.x; w[4 * j + 1] = x.y; w[4 * j + 2] = x.z; w[4 * j + 3] = x.w;
   }
 }
-#endif
 
 // Second 64 B of a slot, only for lanes whose headers can reach past byte 64 (IPv6, IPv4
 // options, VLAN + options) and only when the slot holds them.
@@ -362,25 +333,16 @@ struct rtn_chunk {
 __device__ __forceinline__ rtn_u64 rtn_nchunks(rtn_u32 n) {
   return ((rtn_u64)n + 64u * RTN_CHUNK_GROUPS - 1u) / (64u * RTN_CHUNK_GROUPS);
 }
-#ifndef RTN_RB
-// RTN_REC_BLOCK. Other values are a timing-only switch (the table and PacketDeliver kernels read
-// 64-record blocks): 16 and 32 measured within 1 % of 64 on cfg2 (in-process A/B, one box).
-#define RTN_RB 64u
-#endif
+#define RTN_RB 64u  // RTN_REC_BLOCK (retina_pc.h); the table and PacketDeliver kernels read 64-record blocks
 __device__ __forceinline__ rtn_u64 rtn_rec_slot(rtn_u64 nch, rtn_u64 c, rtn_u32 k) {
   return ((rtn_u64)(k / RTN_RB) * nch + c) * RTN_RB + (k % RTN_RB);
 }
 
 
-// Records leave through a per-wave LDS ring of 256 records (6 KB) as whole 128-record blocks:
-// three full-width 16-B-per-lane stores per 3 KB, every line written whole.
-#ifdef RTN_XPOSE
-#define RTN_RING 128u   // leaves LDS room for the transpose tile
+// Records leave through a per-wave LDS ring of 128 records (3 KB) as whole 64-record blocks:
+// full-width 16-B-per-lane stores, every line written whole.
+#define RTN_RING 128u
 #define RTN_FLUSH 64u
-#else
-#define RTN_RING 256u
-#define RTN_FLUSH 128u
-#endif
 
 __device__ __forceinline__ void rtn_flush(const rtn_args& a, const rtn_u64* ring, const rtn_u64* cring,
                                           const rtn_chunk& ch, rtn_u32 lane, rtn_u32 nrecs) {
@@ -393,44 +355,17 @@ __device__ __forceinline__ void rtn_flush(const rtn_args& a, const rtn_u64* ring
     rtn_v4u* cdst = reinterpret_cast<rtn_v4u*>(a.conn + rtn_rec_slot(nch, ch.rec_base / (64u * RTN_CHUNK_GROUPS), ch.nflushed));
     if (lane < nc) RTN_ST(cdst + (lane / (RTN_RB / 2u)) * nch * (RTN_RB / 2u) + lane % (RTN_RB / 2u), csrc[lane]);
   }
-#ifndef RTN_NO_PAD_TAIL
   // whole 128-B lines only: the block starts line-aligned and the tail is padded with stale ring
   // bytes into the chunk's unused record space (a partial line costs a read-modify-write)
   const rtn_u32 nv4 = ((nrecs * 3u + 1u) / 2u + 7u) & ~7u;
-#else
-  const rtn_u32 nv4 = (nrecs * 3u + 1u) >> 1;  // 24-B records in 16-B lanes (a trailing half lane
-                                               // spills into the chunk's next, unused slot)
-#endif
   const rtn_v4u* src = reinterpret_cast<const rtn_v4u*>(ring) + ((ch.nflushed & (RTN_RING - 1u)) * 3u >> 1);
-#if defined(RTN_EXP_REC_STRIDE)
-  // experiment: record regions RTN_EXP_REC_STRIDE records apart (overlapping: timing only)
-  rtn_v4u* dst = reinterpret_cast<rtn_v4u*>(a.recs + ch.rec_base / (64u * RTN_CHUNK_GROUPS) * RTN_EXP_REC_STRIDE + ch.nflushed);
-#elif defined(RTN_EXP_REC_DENSE)
-  // experiment: records globally dense in flush order (one reservation per block; timing only)
-  rtn_u32 base = 0u;
-  if (lane == 0u) base = atomicAdd(&a.counters[3], (nrecs + 15u) & ~15u);
-  base = __shfl(base, 0);
-  const rtn_u64 cap = (rtn_u64)((a.n + 511u) / 512u) * 512u - 1024u;
-  rtn_v4u* dst = reinterpret_cast<rtn_v4u*>(a.recs + (((rtn_u64)base % cap) & ~15ull));
-#elif defined(RTN_EXP_REC_CHUNK)
-  // experiment: the earlier layout, records dense per chunk at chunk * 512 + k (timing only)
-  rtn_v4u* dst = reinterpret_cast<rtn_v4u*>(a.recs + ch.rec_base + ch.nflushed);
-#elif defined(RTN_EXP_REC_WRAP)
-  // experiment: every chunk's records land in one of RTN_EXP_REC_WRAP regions (L2-resident)
-  rtn_v4u* dst = reinterpret_cast<rtn_v4u*>(a.recs + (ch.rec_base / (64u * RTN_CHUNK_GROUPS) % RTN_EXP_REC_WRAP) * (64u * RTN_CHUNK_GROUPS) + ch.nflushed);
-#else
   // a block of RTN_RB records is RTN_RB * 3 / 2 lanes; a flush (RTN_FLUSH) may span several
   const rtn_u64 nch = rtn_nchunks(a.n);
   rtn_v4u* dst = reinterpret_cast<rtn_v4u*>(a.recs + rtn_rec_slot(nch, ch.rec_base / (64u * RTN_CHUNK_GROUPS), ch.nflushed));
-#endif
 #pragma unroll
   for (rtn_u32 j = 0; j < 3u; ++j) {
     const rtn_u32 k = lane + 64u * j;
-#if defined(RTN_EXP_REC_STRIDE) || defined(RTN_EXP_REC_DENSE) || defined(RTN_EXP_REC_WRAP) || defined(RTN_EXP_REC_CHUNK)
-    if (k < nv4) RTN_ST(dst + k, src[k]);
-#else
     if (k < nv4) RTN_ST(dst + (k / (RTN_RB * 3u / 2u)) * nch * (RTN_RB * 3u / 2u) + k % (RTN_RB * 3u / 2u), src[k]);
-#endif
   }
 }
 
@@ -462,8 +397,11 @@ __device__ __forceinline__ void rtn_group(const rtn_args& a, rtn_u32 g, rtn_u32 
   const bool valid = i < a.n;
   rtn_view v;
   rtn_parse<NW>(w, dl, v);
-  // 64-byte slots: a packet whose headers run past byte 64 cannot be parsed from its slot.
+  // 64-byte slots: a packet whose headers run past byte 64 cannot be parsed from its slot
+  // (RTN_STATUS_HDR_PAST_SLOT); with RTN_BATCH_DL_LE64 asserted no frame may be longer than its
+  // slot (RTN_STATUS_DL_PAST_SLOT).
   if (NW == 16 && (v.v4 || v.v6) && dl > 64u && v.l4off + 20u > 64u) acc.status |= 1u;
+  if (NW == 16 && (a.flags & 8u) && dl > 64u) acc.status |= 2u;
   rtn_u32 act = 0;
   rtn_u64 dm[RTN_DM_WORDS];
 #pragma unroll
@@ -478,9 +416,11 @@ __device__ __forceinline__ void rtn_group(const rtn_args& a, rtn_u32 g, rtn_u32 
   acc.fwd += nfwd;
   acc.bytes += dl;               // lanes past n have dl == 0
   acc.ignored += pc ? 0u : dl;
+  acc.tcp += (rtn_u32)__popcll(__ballot(fwd && v.tcp));
+  acc.tcpb += (fwd && v.tcp) ? dl : 0u;
+  acc.udpb += (fwd && !v.tcp) ? dl : 0u;
   ch.my_pc = lane == k ? pcm : ch.my_pc;
   ch.my_fwd = lane == k ? fwdm : ch.my_fwd;
-#ifndef RTN_EXP_NO_STORES
   if (fwd) {
     const rtn_u32 r = ch.nrec + (rtn_u32)__popcll(fwdm & lane_lt);
     const bool tcp = v.tcp;
@@ -562,11 +502,7 @@ __device__ __forceinline__ void rtn_group(const rtn_args& a, rtn_u32 g, rtn_u32 
   }
   ch.nrec += nfwd;
   // IPv6 source/destination addresses, ranked among the chunk's forwarded IPv6 frames
-#ifndef RTN_EXP_NO_ADDR6
   const bool six = fwd && v.v6 && (a.flags & 1u);
-#else
-  const bool six = false;
-#endif
   const rtn_u64 m6 = __ballot(six);
   if (six) {
     const rtn_u32 r6 = ch.nv6 + (rtn_u32)__popcll(m6 & lane_lt);
@@ -594,7 +530,6 @@ __device__ __forceinline__ void rtn_group(const rtn_args& a, rtn_u32 g, rtn_u32 
     ch.nflushed += RTN_FLUSH;
     rtn_wave_sync();
   }
-#endif
 #if RTN_DELIVER_WORDS > 0
   {
     rtn_u64 any = 0;
@@ -604,11 +539,7 @@ __device__ __forceinline__ void rtn_group(const rtn_args& a, rtn_u32 g, rtn_u32 
     const rtn_u64 dlvm = __ballot(d);
     ch.my_dlv = lane == k ? dlvm : ch.my_dlv;
     acc.dlv += (rtn_u32)__popcll(dlvm);
-#ifdef RTN_EXP_NO_DLV
-    if (false) {
-#else
     if (d) {
-#endif
       const rtn_u64 slot_i = ch.rec_base + ch.ndlv + (rtn_u32)__popcll(dlvm & lane_lt);
       rtn_u64* dp = a.dlv_recs + slot_i * (1u + RTN_DELIVER_WORDS);
       RTN_ST8(dp, (rtn_u64)i);
@@ -621,9 +552,8 @@ __device__ __forceinline__ void rtn_group(const rtn_args& a, rtn_u32 g, rtn_u32 
 }
 
 // Chunk loop. Each wave takes chunks wave_g, wave_g + nwaves, ... and walks a chunk's groups in
-// order, RTN_UNROLL groups per iteration so that all of their loads are in flight before the
-// first is parsed. MODE: RTN_S64 (64-byte slots), RTN_SPLIT (64-byte slots + ext slab holding
-// bytes 64..127), RTN_MONO (monolithic slots of any stride >= 64).
+// order. MODE: RTN_S64 (64-byte slots), RTN_SPLIT (64-byte slots + ext slab holding bytes
+// 64..127), RTN_MONO (monolithic slots of any stride >= 64).
 #define RTN_S64 0
 #define RTN_SPLIT 1
 #define RTN_MONO 2
@@ -636,7 +566,7 @@ __device__ __forceinline__ void rtn_run(const rtn_args& a) {
   const rtn_u32 nchunks = (nw + RTN_CHUNK_GROUPS - 1u) / RTN_CHUNK_GROUPS;
   const rtn_u64 lane_lt = (lane == 0u) ? 0ull : (~0ull >> (64u - lane));
   constexpr bool slots64 = MODE != RTN_MONO;
-  rtn_acc acc = {0u, 0u, 0u, 0u, 0ull, 0ull};
+  rtn_acc acc = {0u, 0u, 0u, 0u, 0u, 0ull, 0ull, 0ull, 0ull};
   __shared__ __attribute__((aligned(16))) rtn_u64 rtn_ring[4][RTN_RING * 3u];
   rtn_u64* ring = rtn_ring[threadIdx.x >> 6];
   __shared__ __attribute__((aligned(16))) rtn_u64 rtn_cring[4][RTN_RING];  // connection-stage entries
@@ -644,114 +574,48 @@ __device__ __forceinline__ void rtn_run(const rtn_args& a) {
   constexpr bool stage6 = MODE != RTN_S64;  // 64-byte slots rarely forward IPv6 (only short UDP)
   __shared__ __attribute__((aligned(16))) rtn_v4u rtn_ring6[4][stage6 ? RTN_RING6 * 2u : 1u];
   rtn_v4u* ring6 = rtn_ring6[threadIdx.x >> 6];
-#ifdef RTN_XPOSE
-  __shared__ __attribute__((aligned(16))) rtn_u32 rtn_tile[4][64 * RTN_XPITCH];
+  __shared__ __attribute__((aligned(16))) rtn_u32 rtn_tile[4][slots64 ? 64 * RTN_XPITCH : 1];
   rtn_u32* tile = rtn_tile[threadIdx.x >> 6];
-#endif
   for (rtn_u32 c = wave_g; c < nchunks; c += nwaves) {
     const rtn_u32 gb = c * RTN_CHUNK_GROUPS;
     const rtn_u32 ge = gb + RTN_CHUNK_GROUPS < nw ? gb + RTN_CHUNK_GROUPS : nw;
     rtn_chunk ch = {(rtn_u64)c * (64u * RTN_CHUNK_GROUPS), 0u, 0u, 0u, 0u, 0u, 0ull, 0ull, 0ull};
-    for (rtn_u32 g0 = gb; g0 < ge; g0 += RTN_UNROLL) {
-      rtn_u32 lo[RTN_UNROLL][16], dl[RTN_UNROLL];
-#ifdef RTN_XPOSE
-      rtn_v4u q[RTN_UNROLL][4];
+    for (rtn_u32 g = gb; g < ge; ++g) {
+      rtn_u32 lo[16], dl;
       if (slots64) {
-#pragma unroll
-        for (int u = 0; u < RTN_UNROLL; ++u) {
-          const rtn_u32 g = g0 + u;
-          if (u == 0 || g < ge) rtn_load_group(a, g, lane, q[u], dl[u]);
-        }
-      } else
-#endif
-      {
-#pragma unroll
-        for (int u = 0; u < RTN_UNROLL; ++u) {
-          const rtn_u32 g = g0 + u;
-          if (u == 0 || g < ge) rtn_load_lo(a, g * 64u + lane, lo[u], dl[u]);
-        }
+        rtn_v4u q[4];
+        rtn_load_group(a, g, lane, q, dl);
+        rtn_xpose(tile, lane, q, lo);
+      } else {
+        rtn_load_lo(a, g * 64u + lane, lo, dl);
       }
-#ifdef RTN_HI_EARLY
-      // experiment: transpose and issue every group's second-half loads before parsing any
-      rtn_u32 wh[RTN_UNROLL][16];
-      if (MODE != RTN_S64) {
+      if (MODE == RTN_S64) {
+        rtn_group<16, stage6>(a, g, g - gb, lane, lane_lt, lo, dl, ring, cring, ring6, ch, acc);
+      } else {
+        rtn_u32 w[32];
 #pragma unroll
-        for (int u = 0; u < RTN_UNROLL; ++u) {
-          const rtn_u32 g = g0 + u;
-          if (u > 0 && g >= ge) break;
-#ifdef RTN_XPOSE
-          if (slots64) rtn_xpose(tile, lane, q[u], lo[u]);
-#endif
+        for (int j = 0; j < 16; ++j) w[j] = lo[j];
 #pragma unroll
-          for (int j = 0; j < 16; ++j) wh[u][j] = 0u;
-          if (rtn_need_hi(lo[u], dl[u])) {
-            const rtn_v4u* hi = MODE == RTN_SPLIT
-                                    ? reinterpret_cast<const rtn_v4u*>(a.ext + (rtn_u64)(g * 64u + lane) * 64u)
-                                    : reinterpret_cast<const rtn_v4u*>(a.slab + (rtn_u64)(g * 64u + lane) * a.stride) + 4;
+        for (int j = 16; j < 32; ++j) w[j] = 0u;
+        if (rtn_need_hi(lo, dl)) {
+          // bytes 64..127: the ext slot (split layout) or the slot's second half (monolithic)
+          const rtn_v4u* hi = MODE == RTN_SPLIT
+                                  ? reinterpret_cast<const rtn_v4u*>(a.ext + (rtn_u64)(g * 64u + lane) * 64u)
+                                  : reinterpret_cast<const rtn_v4u*>(a.slab + (rtn_u64)(g * 64u + lane) * a.stride) + 4;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              const rtn_v4u x = RTN_LD(hi + j);
-              wh[u][4 * j + 0] = x.x; wh[u][4 * j + 1] = x.y; wh[u][4 * j + 2] = x.z; wh[u][4 * j + 3] = x.w;
-            }
+          for (int j = 0; j < 4; ++j) {
+            const rtn_v4u x = hi[j];
+            w[16 + 4 * j + 0] = x.x; w[16 + 4 * j + 1] = x.y; w[16 + 4 * j + 2] = x.z; w[16 + 4 * j + 3] = x.w;
           }
         }
-#pragma unroll
-        for (int u = 0; u < RTN_UNROLL; ++u) {
-          const rtn_u32 g = g0 + u;
-          if (u > 0 && g >= ge) break;
-          rtn_u32 w[32];
-#pragma unroll
-          for (int j = 0; j < 16; ++j) { w[j] = lo[u][j]; w[16 + j] = wh[u][j]; }
-          rtn_group<32, stage6>(a, g, g - gb, lane, lane_lt, w, dl[u], ring, cring, ring6, ch, acc);
-        }
-        continue;
-      }
-#endif
-#pragma unroll
-      for (int u = 0; u < RTN_UNROLL; ++u) {
-        const rtn_u32 g = g0 + u;
-        if (u > 0 && g >= ge) break;
-#ifdef RTN_XPOSE
-        if (slots64) rtn_xpose(tile, lane, q[u], lo[u]);
-#endif
-        if (MODE == RTN_S64) {
-#ifdef RTN_EXP_READ_ONLY
-          // experiment: the production access pattern + transpose, no parse/filter/stores
-          rtn_u32 x = dl[u];
-#pragma unroll
-          for (int j = 0; j < 16; ++j) x ^= lo[u][j];
-          acc.status |= (x == 0x9E3779B9u) ? 2u : 0u;
-#else
-          rtn_group<16, stage6>(a, g, g - gb, lane, lane_lt, lo[u], dl[u], ring, cring, ring6, ch, acc);
-#endif
-        } else {
-          rtn_u32 w[32];
-#pragma unroll
-          for (int j = 0; j < 16; ++j) w[j] = lo[u][j];
-#pragma unroll
-          for (int j = 16; j < 32; ++j) w[j] = 0u;
-          if (rtn_need_hi(lo[u], dl[u])) {
-            // bytes 64..127: the ext slot (split layout) or the slot's second half (monolithic)
-            const rtn_v4u* hi = MODE == RTN_SPLIT
-                                    ? reinterpret_cast<const rtn_v4u*>(a.ext + (rtn_u64)(g * 64u + lane) * 64u)
-                                    : reinterpret_cast<const rtn_v4u*>(a.slab + (rtn_u64)(g * 64u + lane) * a.stride) + 4;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              const rtn_v4u x = RTN_LD(hi + j);
-              w[16 + 4 * j + 0] = x.x; w[16 + 4 * j + 1] = x.y; w[16 + 4 * j + 2] = x.z; w[16 + 4 * j + 3] = x.w;
-            }
-          }
-          rtn_group<32, stage6>(a, g, g - gb, lane, lane_lt, w, dl[u], ring, cring, ring6, ch, acc);
-        }
+        rtn_group<32, stage6>(a, g, g - gb, lane, lane_lt, w, dl, ring, cring, ring6, ch, acc);
       }
     }
     // chunk epilogue: the partial last record block, then one store per bitmap for the chunk
-#ifndef RTN_EXP_NO_STORES
     rtn_wave_sync();
     rtn_flush(a, ring, cring, ch, lane, ch.nrec - ch.nflushed);
     if (stage6) rtn_flush6(a, ring6, ch, lane, ch.nv6 - ch.nv6flushed);
     rtn_wave_sync();
-#endif
     if (lane < ge - gb) {
       RTN_ST8(a.pc_bm + gb + lane, ch.my_pc);
       RTN_ST8(a.fwd_bm + gb + lane, ch.my_fwd);
@@ -760,15 +624,17 @@ __device__ __forceinline__ void rtn_run(const rtn_args& a) {
 #endif
     }
   }
-  // one set of atomics per wave
-  const rtn_u64 st = __ballot(acc.status != 0u);
-  if (lane == 0u && st) atomicOr(&a.counters[3], 1u);
+  // one set of atomics per wave: status bits always (RTN_STATUS_*), totals when requested
+  const rtn_u32 st = (__ballot((acc.status & 1u) != 0u) ? 1u : 0u) | (__ballot((acc.status & 2u) != 0u) ? 2u : 0u);
+  if (lane == 0u && st) atomicOr(&a.counters[3], st);
   if (!(a.flags & 2u)) return;
-  rtn_u64 bytes = acc.bytes, ignored = acc.ignored;
+  rtn_u64 bytes = acc.bytes, ignored = acc.ignored, tcpb = acc.tcpb, udpb = acc.udpb;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
     bytes += __shfl_xor(bytes, off);
     ignored += __shfl_xor(ignored, off);
+    tcpb += __shfl_xor(tcpb, off);
+    udpb += __shfl_xor(udpb, off);
   }
   if (lane == 0u) {
     if (acc.pc) atomicAdd(&a.counters[0], acc.pc);
@@ -776,53 +642,16 @@ __device__ __forceinline__ void rtn_run(const rtn_args& a) {
     if (acc.dlv) atomicAdd(&a.counters[2], acc.dlv);
     if (bytes) atomicAdd(reinterpret_cast<unsigned long long*>(a.counters + 4), bytes);
     if (ignored) atomicAdd(reinterpret_cast<unsigned long long*>(a.counters + 6), ignored);
+    if (acc.tcp) atomicAdd(&a.counters[8], acc.tcp);
+    if (acc.fwd - acc.tcp) atomicAdd(&a.counters[9], acc.fwd - acc.tcp);
+    if (tcpb) atomicAdd(reinterpret_cast<unsigned long long*>(a.counters + 10), tcpb);
+    if (udpb) atomicAdd(reinterpret_cast<unsigned long long*>(a.counters + 12), udpb);
   }
 }
 
-#ifdef RTN_EXP_CEILING
-// Experiment only: fully coalesced read of the slab (16 B per lane), the HBM-read ceiling.
-#define RTN_BODY(S64)                                                                                 \
-  {                                                                                                   \
-    const rtn_u64 n16 = (rtn_u64)a.n * a.stride / 16u;                                                \
-    const rtn_v4u* p = reinterpret_cast<const rtn_v4u*>(a.slab);                                      \
-    rtn_u32 x = 0;                                                                                    \
-    for (rtn_u64 k = blockIdx.x * (rtn_u64)blockDim.x + threadIdx.x; k < n16;                         \
-         k += (rtn_u64)gridDim.x * blockDim.x) {                                                      \
-      const rtn_v4u v = RTN_LD(p + k);                                            \
-      x ^= v.x + v.y + v.z + v.w;                                                                     \
-    }                                                                                                 \
-    if (x == 0x9E3779B9u) a.counters[3] = x;                                                          \
-  }
-#elif defined(RTN_EXP_LANE_READ)
-// Experiment only: the production per-lane access pattern (RTN_EXP_LANE_READ dwordx4 per lane
-// of its own slot), read only.
-__device__ __forceinline__ void rtn_lane_read(const rtn_args& a) {
-  const rtn_u32 lane = threadIdx.x & 63u;
-  const rtn_u32 wave_g = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
-  const rtn_u32 nwaves = (gridDim.x * blockDim.x) >> 6;
-  const rtn_u32 nw = (a.n + 63u) >> 6;
-  rtn_u32 x = 0;
-  for (rtn_u32 g = wave_g; g < nw; g += nwaves) {
-    const rtn_u32 i = g * 64u + lane;
-    const rtn_u32 ic = i < a.n ? i : a.n - 1u;
-    const rtn_v4u* slot = reinterpret_cast<const rtn_v4u*>(a.slab + (rtn_u64)ic * a.stride);
-#pragma unroll
-    for (int k = 0; k < RTN_EXP_LANE_READ; ++k) {
-      const rtn_v4u v = RTN_LD(slot + k);
-      x ^= v.x + v.y + v.z + v.w;
-    }
-    x += a.dlen[ic];
-  }
-  if (x == 0x9E3779B9u) a.counters[3] = x;
-}
-#define RTN_BODY(S64) { rtn_lane_read(a); }
-#else
-#define RTN_BODY(MODE) { rtn_run<MODE>(a); }
-#endif
-
-extern "C" __global__ void __launch_bounds__(256) rtn_pc_kernel(rtn_args a) RTN_BODY(RTN_MONO)
-extern "C" __global__ void __launch_bounds__(256) rtn_pc_kernel_s64(rtn_args a) RTN_BODY(RTN_S64)
-extern "C" __global__ void __launch_bounds__(256) rtn_pc_kernel_split(rtn_args a) RTN_BODY(RTN_SPLIT)
+extern "C" __global__ void __launch_bounds__(256) rtn_pc_kernel(rtn_args a) { rtn_run<RTN_MONO>(a); }
+extern "C" __global__ void __launch_bounds__(256) rtn_pc_kernel_s64(rtn_args a) { rtn_run<RTN_S64>(a); }
+extern "C" __global__ void __launch_bounds__(256) rtn_pc_kernel_split(rtn_args a) { rtn_run<RTN_SPLIT>(a); }
 
 // ---------------------------------------------------------------------------------------------
 // PacketDeliver filter (rtn_pd_run): the generated `packet_deliver` (filtergen/src/lib.rs:357-362,
@@ -857,11 +686,9 @@ struct rtn_pd_args {
   rtn_u64* pd_bm;              // [ceil(n/64)]: the frame has at least one delivery
 };
 
-#ifndef RTN_PD_GPW
 // groups (64 frames) per wave (1, 2, 4 and 8 measured within 3 % on cfg2: 0.40-0.41 ms; 1 is
 // the fastest)
 #define RTN_PD_GPW 1u
-#endif
 #define RTN_PD_THREADS (512u / RTN_PD_GPW)
 
 // One block per 512-frame chunk, RTN_PD_GPW 64-frame groups per wave, one lane per frame of each.
@@ -986,13 +813,9 @@ extern "C" __global__ void __launch_bounds__(RTN_PD_THREADS) rtn_pd_kernel(rtn_p
     if (dl) {
 #pragma unroll
       for (int j = 0; j < RTN_PD_S; ++j) {
-#ifndef RTN_PD_TEMPORAL
-        // written once, read by the host or a later launch: non-temporal (cfg2 PacketDeliver
+// written once, read by the host or a later launch: non-temporal (cfg2 PacketDeliver
         // 0.4387 -> 0.4177 ms, in-process A/B on one box)
         __builtin_nontemporal_store(cnt[j], a.counts + r[u] * RTN_PD_S + j);
-#else
-        a.counts[r[u] * RTN_PD_S + j] = cnt[j];
-#endif
       }
     }
   }

@@ -9,6 +9,8 @@
 
 #include <cstdlib>
 #include <cstring>
+#include <fstream>
+#include <sstream>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -44,9 +46,10 @@ size_t copy_text(const std::string& s, char* buf, size_t cap) {
 }
 
 std::string env_defines();
+std::string kernel_template();
 
 std::string build_source(const rtn::PacketProgram& prog) {
-  const std::string tpl = kPcKernelSrc;
+  const std::string tpl = kernel_template();
   const std::string marker = "//@@RTN_FILTER@@";
   size_t at = tpl.find(marker);
   std::string head = "#define RTN_DELIVER_WORDS " + std::to_string(prog.deliver_words()) + "\n" +
@@ -63,9 +66,25 @@ std::string build_source(const rtn::PacketProgram& prog) {
   return src.substr(0, dat) + prog.hip_pd_body + src.substr(dat + dmarker.size());
 }
 
-// Kernel variants for experiments (RTN_KERNEL_DEFINES="A,B=1"); never set in production runs.
+// Kernel experiments: only a library built with -DRTN_EXPERIMENTS (tools/build_experiments.py)
+// reads RTN_KERNEL_DEFINES="A,B=1" (prepended #defines) and RTN_KERNEL_TEMPLATE=<file> (a
+// variant of pc_kernel.hip). The product library has neither, so no environment variable can
+// change what a kernel computes or where it writes.
+std::string kernel_template() {
+#ifdef RTN_EXPERIMENTS
+  if (const char* f = getenv("RTN_KERNEL_TEMPLATE")) {
+    std::ifstream in(f);
+    std::stringstream ss;
+    ss << in.rdbuf();
+    if (in && !ss.str().empty()) return ss.str();
+  }
+#endif
+  return kPcKernelSrc;
+}
+
 std::string env_defines() {
   std::string head;
+#ifdef RTN_EXPERIMENTS
   if (const char* d = getenv("RTN_KERNEL_DEFINES")) {
     std::string all = d, tok;
     for (size_t k = 0; k <= all.size(); ++k) {
@@ -77,6 +96,7 @@ std::string env_defines() {
       }
     }
   }
+#endif
   return head;
 }
 
@@ -198,7 +218,7 @@ struct KArgs {
 };
 
 // Groups per wave of a kernel (RTN_PD_GPW / RTN_CT_GPW): the default, unless an RTN_KERNEL_DEFINES
-// experiment overrides it (the launch's block size follows it).
+// experiment (experiments build only) overrides it (the launch's block size follows it).
 uint32_t groups_per_wave(const char* name, uint32_t dflt) {
   const std::string d = env_defines(), key = std::string("#define ") + name + " ";
   size_t at = d.find(key);
@@ -241,7 +261,14 @@ struct rtn_pc {
   hipFunction_t fn_split = nullptr;  // rtn_pc_kernel_split: 64-byte slots + ext
   hipFunction_t fn_pd = nullptr;     // rtn_pd_kernel: the PacketDeliver filter (rtn_pd_run)
   uint32_t blocks = 0;
-  uint32_t* scratch_counters = nullptr;  // used when the caller passes no counters
+  // used when the caller passes no counters: word RTN_CNT_STATUS accumulates the status bits of
+  // such runs until rtn_pc_take_status reads and clears them (the other words are never read)
+  uint32_t* scratch_counters = nullptr;
+  ~rtn_pc() {
+    if (scratch_counters) (void)hipFree(scratch_counters);
+    if (module) (void)hipModuleUnload(module);
+    delete owned;
+  }
 };
 
 extern "C" {
@@ -432,9 +459,13 @@ int32_t rtn_pc_create_from_program(rtn_program_t* p, int device, rtn_pc_t** out)
   if (e != hipSuccess) return fail(RTN_EDEVICE, std::string("hipModuleGetFunction: ") + hipGetErrorString(e));
   e = hipModuleGetFunction(&pc->fn_pd, pc->module, "rtn_pd_kernel");
   if (e != hipSuccess) return fail(RTN_EDEVICE, std::string("hipModuleGetFunction: ") + hipGetErrorString(e));
-  e = hipMalloc(&pc->scratch_counters, 32);
+  e = hipMalloc(&pc->scratch_counters, RTN_COUNTERS_BYTES);
   if (e != hipSuccess) return fail(RTN_EDEVICE, std::string("hipMalloc: ") + hipGetErrorString(e));
+  e = hipMemset(pc->scratch_counters, 0, RTN_COUNTERS_BYTES);
+  if (e != hipSuccess) return fail(RTN_EDEVICE, std::string("hipMemset: ") + hipGetErrorString(e));
+#ifdef RTN_EXPERIMENTS
   if (const char* g = getenv("RTN_GRID")) pc->blocks = (uint32_t)strtoul(g, nullptr, 10);
+#endif
   *out = pc.release();
   return RTN_OK;
 }
@@ -445,7 +476,7 @@ int32_t rtn_pc_create(const char* spec, size_t len, int device, rtn_pc_t** out) 
   if (rc) return rc;
   rc = rtn_pc_create_from_program(p, device, out);
   if (rc) {
-    rtn_program_destroy(p);
+    rtn_program_destroy(p);  // (a failed create released everything it had set up)
     return rc;
   }
   (*out)->owned = p;
@@ -460,6 +491,8 @@ int32_t rtn_pc_set_grid(rtn_pc_t* pc, uint32_t blocks) {
 
 int32_t rtn_pc_run(rtn_pc_t* pc, const rtn_batch_t* in, rtn_pc_out_t* out, void* stream) {
   if (!pc || !in || !out) return fail(RTN_EINVAL, "null argument");
+  if (in->n > RTN_MAX_FRAMES) return fail(RTN_EINVAL, "batch larger than RTN_MAX_FRAMES");
+  if (in->flags & ~RTN_BATCH_DL_LE64) return fail(RTN_EINVAL, "unknown rtn_batch_t flags");
   if (in->n == 0) return RTN_OK;
   if (!in->slab || !in->data_len) return fail(RTN_EINVAL, "batch slab/data_len missing");
   if (in->stride < 64 || in->stride % 64 != 0) return fail(RTN_EINVAL, "stride must be a positive multiple of 64");
@@ -468,6 +501,10 @@ int32_t rtn_pc_run(rtn_pc_t* pc, const rtn_batch_t* in, rtn_pc_out_t* out, void*
   if (in->ext && (reinterpret_cast<uintptr_t>(in->ext) & 15u) != 0)
     return fail(RTN_EINVAL, "ext must be 16-byte aligned");
   if (!out->pc_bitmap || !out->fwd_bitmap || !out->l4) return fail(RTN_EINVAL, "pc_bitmap/fwd_bitmap/l4 required");
+  // 64-byte slots without ext: the caller must either guarantee data_len <= 64 or receive the
+  // status word (RTN_STATUS_HDR_PAST_SLOT), so that a frame parsed past its slot is never silent
+  if (in->stride == 64 && !in->ext && !(in->flags & RTN_BATCH_DL_LE64) && !out->counters)
+    return fail(RTN_EINVAL, "64-byte slots without ext need RTN_BATCH_DL_LE64 (every data_len <= 64) or counters");
   // record arrays leave in 16-B-per-lane stores
   for (const void* o : {(const void*)out->l4, (const void*)out->addr6, (const void*)out->conn})
     if ((reinterpret_cast<uintptr_t>(o) & 15u) != 0) return fail(RTN_EINVAL, "l4/addr6/conn must be 16-byte aligned");
@@ -479,7 +516,7 @@ int32_t rtn_pc_run(rtn_pc_t* pc, const rtn_batch_t* in, rtn_pc_out_t* out, void*
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   hipError_t e;
   if (out->counters) {
-    e = hipMemsetAsync(out->counters, 0, 32, s);
+    e = hipMemsetAsync(out->counters, 0, RTN_COUNTERS_BYTES, s);
     if (e != hipSuccess) return fail(RTN_EDEVICE, std::string("hipMemsetAsync: ") + hipGetErrorString(e));
   }
   KArgs a;
@@ -487,7 +524,8 @@ int32_t rtn_pc_run(rtn_pc_t* pc, const rtn_batch_t* in, rtn_pc_out_t* out, void*
   a.stride = in->stride;
   a.dlen = in->data_len;
   a.n = in->n;
-  a.flags = (out->addr6 ? 1u : 0u) | (out->counters ? 2u : 0u) | (out->conn ? 4u : 0u);
+  a.flags = (out->addr6 ? 1u : 0u) | (out->counters ? 2u : 0u) | (out->conn ? 4u : 0u) |
+            ((in->flags & RTN_BATCH_DL_LE64) ? 8u : 0u);
   a.pc_bm = out->pc_bitmap;
   a.fwd_bm = out->fwd_bitmap;
   a.recs = out->l4;
@@ -516,6 +554,7 @@ int32_t rtn_pd_run(rtn_pc_t* pc, const rtn_pc_out_t* out, const rtn_ct_entry_t* 
                    uint32_t n, const uint32_t* state, uint32_t state_slots, uint32_t* counts, uint64_t* pd_bitmap,
                    void* stream) {
   if (!pc || !out || !ct || !data_len || !pd_bitmap) return fail(RTN_EINVAL, "null argument");
+  if (n > RTN_MAX_FRAMES) return fail(RTN_EINVAL, "batch larger than RTN_MAX_FRAMES");
   if (n == 0) return RTN_OK;
   if (!out->fwd_bitmap || !out->l4 || !out->addr6 || !out->conn)
     return fail(RTN_EINVAL, "fwd_bitmap, l4, addr6 and conn required");
@@ -545,17 +584,24 @@ int32_t rtn_pd_run(rtn_pc_t* pc, const rtn_pc_out_t* out, const rtn_ct_entry_t* 
   return RTN_OK;
 }
 
+int32_t rtn_pc_take_status(rtn_pc_t* pc, uint32_t* status) {
+  if (!pc || !status) return fail(RTN_EINVAL, "null argument");
+  hipError_t e = hipSetDevice(pc->device);
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  if (e == hipSuccess) e = hipMemcpy(status, pc->scratch_counters + RTN_CNT_STATUS, 4, hipMemcpyDeviceToHost);
+  if (e == hipSuccess) e = hipMemset(pc->scratch_counters + RTN_CNT_STATUS, 0, 4);
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  return e == hipSuccess ? RTN_OK : fail(RTN_EDEVICE, std::string("rtn_pc_take_status: ") + hipGetErrorString(e));
+}
+
 int32_t rtn_pc_destroy(rtn_pc_t* pc) {
-  if (!pc) return RTN_OK;
-  if (pc->scratch_counters) (void)hipFree(pc->scratch_counters);
-  if (pc->module) (void)hipModuleUnload(pc->module);
-  if (pc->owned) rtn_program_destroy(pc->owned);
   delete pc;
   return RTN_OK;
 }
 
-size_t rtn_out_bitmap_bytes(uint32_t n) { return (size_t)((n + 63u) / 64u) * 8u; }
-static size_t chunked(uint32_t n) { return (size_t)((n + RTN_CHUNK_FRAMES - 1u) / RTN_CHUNK_FRAMES) * RTN_CHUNK_FRAMES; }
+// sizes in 64-bit arithmetic (n up to 2^32 - 1 must not wrap)
+size_t rtn_out_bitmap_bytes(uint32_t n) { return (((size_t)n + 63u) / 64u) * 8u; }
+static size_t chunked(uint32_t n) { return (((size_t)n + RTN_CHUNK_FRAMES - 1u) / RTN_CHUNK_FRAMES) * RTN_CHUNK_FRAMES; }
 static_assert(sizeof(rtn_l4ctx_t) == 24, "rtn_l4ctx_t is 24 bytes");
 size_t rtn_out_l4_bytes(uint32_t n) { return chunked(n) * sizeof(rtn_l4ctx_t); }
 size_t rtn_out_addr6_bytes(uint32_t n) { return chunked(n) * 32u; }
@@ -584,6 +630,12 @@ struct rtn_ct {
   uint32_t* live = nullptr;  // [64] counters, live = their sum (mod 2^32)
   hipModule_t module = nullptr;
   hipFunction_t insert = nullptr, lookup = nullptr, remove = nullptr, clear = nullptr, rehash = nullptr;
+  ~rtn_ct() {
+    if (table) (void)hipFree(table);
+    if (occ) (void)hipFree(occ);
+    if (live) (void)hipFree(live);
+    if (module) (void)hipModuleUnload(module);
+  }
 };
 
 namespace {
@@ -672,17 +724,13 @@ int32_t rtn_ct_create(int device, uint32_t capacity_log2, uint32_t max_connectio
 }
 
 int32_t rtn_ct_destroy(rtn_ct_t* ct) {
-  if (!ct) return RTN_OK;
-  if (ct->table) (void)hipFree(ct->table);
-  if (ct->occ) (void)hipFree(ct->occ);
-  if (ct->live) (void)hipFree(ct->live);
-  if (ct->module) (void)hipModuleUnload(ct->module);
   delete ct;
   return RTN_OK;
 }
 
 int32_t rtn_ct_process(rtn_ct_t* ct, const rtn_pc_out_t* pc, uint32_t n, rtn_ct_entry_t* out, void* stream) {
   if (!ct || !pc || !out) return fail(RTN_EINVAL, "null argument");
+  if (n > RTN_MAX_FRAMES) return fail(RTN_EINVAL, "batch larger than RTN_MAX_FRAMES");
   if (n == 0) return RTN_OK;
   if (!pc->fwd_bitmap || !pc->l4 || !pc->conn) return fail(RTN_EINVAL, "rtn_pc_out_t needs fwd_bitmap, l4 and conn");
   if (!pc->addr6) return fail(RTN_EINVAL, "rtn_pc_out_t needs addr6 (IPv6 keys)");
@@ -701,9 +749,13 @@ int32_t rtn_ct_process(rtn_ct_t* ct, const rtn_pc_out_t* pc, uint32_t n, rtn_ct_
   a.epoch = ++ct->epoch;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   // Admission against max_connections on the device: one reservation atomic per block that
-  // opens connections (RTN_CT_SPREAD_COUNTERS=1 in the environment selects the unchecked variant
-  // with spread counters, for experiments).
+  // opens connections (RTN_CT_SPREAD_COUNTERS=1 selects the unchecked variant with spread
+  // counters in the experiments build only).
+#ifdef RTN_EXPERIMENTS
   static const bool spread = getenv("RTN_CT_SPREAD_COUNTERS") != nullptr;
+#else
+  const bool spread = false;
+#endif
   a.check = spread ? 0u : 1u;
   const uint32_t chunks = (n + RTN_CHUNK_FRAMES - 1u) / RTN_CHUNK_FRAMES;  // one 512-thread block each
   void* p[] = {&a};

@@ -30,7 +30,15 @@ class FilterError(RetinaError):
 
 class _Batch(C.Structure):
     _fields_ = [("slab", C.c_void_p), ("stride", C.c_uint64), ("data_len", C.c_void_p),
-                ("n", C.c_uint32), ("core_id", C.c_uint32), ("ext", C.c_void_p)]
+                ("n", C.c_uint32), ("core_id", C.c_uint32), ("ext", C.c_void_p), ("flags", C.c_uint32),
+                ("reserved", C.c_uint32)]
+
+
+BATCH_DL_LE64 = 1          # RTN_BATCH_DL_LE64
+STATUS_HDR_PAST_SLOT = 1   # RTN_STATUS_HDR_PAST_SLOT
+STATUS_DL_PAST_SLOT = 2    # RTN_STATUS_DL_PAST_SLOT
+COUNTERS_BYTES = 64        # RTN_COUNTERS_BYTES
+MAX_FRAMES = 1 << 31       # RTN_MAX_FRAMES
 
 
 class _Out(C.Structure):
@@ -72,6 +80,7 @@ EXPORTS = {
     "rtn_pc_create_from_program": (C.c_int32, [C.c_void_p, C.c_int, C.POINTER(C.c_void_p)]),
     "rtn_pc_run": (C.c_int32, [C.c_void_p, C.POINTER(_Batch), C.POINTER(_Out), C.c_void_p]),
     "rtn_pc_set_grid": (C.c_int32, [C.c_void_p, C.c_uint32]),
+    "rtn_pc_take_status": (C.c_int32, [C.c_void_p, C.POINTER(C.c_uint32)]),
     "rtn_pc_destroy": (C.c_int32, [C.c_void_p]),
     "rtn_out_bitmap_bytes": (C.c_size_t, [C.c_uint32]),
     "rtn_out_l4_bytes": (C.c_size_t, [C.c_uint32]),
@@ -289,6 +298,16 @@ class PCOutputs:
         """[pc, fwd, dlv, status] (uint32)."""
         return self.counters.cpu().numpy().view(np.uint32)[:4]
 
+    def stats_host(self) -> dict:
+        """The counters block under the reference's stats names (core/src/stats/mod.rs:9-27), as
+        rx_core.rs:127-139 and Subscription::process_packet (subscription/mod.rs:102-111) would
+        have counted this batch."""
+        w = self.counters.cpu().numpy().view(np.uint32)
+        q = w.view(np.uint64)
+        return {"TOTAL_PKT": int(self.n), "TOTAL_BYTE": int(q[2]),
+                "IGNORED_BY_PACKET_FILTER_PKT": int(self.n) - int(w[0]), "IGNORED_BY_PACKET_FILTER_BYTE": int(q[3]),
+                "TCP_PKT": int(w[8]), "UDP_PKT": int(w[9]), "TCP_BYTE": int(q[5]), "UDP_BYTE": int(q[6])}
+
     def byte_counters_host(self) -> tuple[int, int]:
         """(data_len sum of all frames, data_len sum of the frames not accepted)."""
         b = self.counters.cpu().numpy().view(np.uint64)
@@ -388,6 +407,12 @@ class PacketContinue:
     def set_grid(self, blocks: int) -> None:
         _check(lib().rtn_pc_set_grid(self._h, blocks))
 
+    def take_status(self) -> int:
+        """RTN_STATUS_* bits raised by runs without counters since the last call (synchronizes)."""
+        st = C.c_uint32()
+        _check(lib().rtn_pc_take_status(self._h, C.byref(st)))
+        return int(st.value)
+
     def alloc_outputs(self, n: int, addr6: bool = True, counters: bool = True, conn: bool = False) -> PCOutputs:
         import torch
 
@@ -403,7 +428,7 @@ class PacketContinue:
             addr6=u8(L.rtn_out_addr6_bytes(n)) if addr6 else None,
             dlv_bitmap=u8(L.rtn_out_bitmap_bytes(n)) if dw else None,
             dlv_records=u8(L.rtn_out_dlv_bytes(n, dw)) if dw else None,
-            counters=torch.zeros(32, dtype=torch.uint8, device=dev) if counters else None,
+            counters=torch.zeros(COUNTERS_BYTES, dtype=torch.uint8, device=dev) if counters else None,
             deliver_words=dw,
             conn=u8(L.rtn_out_conn_bytes(n)) if conn else None,
             conn_dlv=u8(L.rtn_out_conn_dlv_bytes(n, self.conn_words)) if conn and self.conn_words else None,
@@ -411,9 +436,11 @@ class PacketContinue:
         )
 
     def run(self, slab, stride: int, data_len, n: int | None = None, out: PCOutputs | None = None,
-            stream=None, core_id: int = 0, ext=None) -> PCOutputs:
+            stream=None, core_id: int = 0, ext=None, dl_le64: bool = False) -> PCOutputs:
         """One rtn_pc_run. `ext` (device uint8, 64 B per frame) selects the split layout: `slab`
-        then holds bytes [0, 64) of every frame (stride 64) and `ext` bytes [64, 128)."""
+        then holds bytes [0, 64) of every frame (stride 64) and `ext` bytes [64, 128).
+        dl_le64 asserts that every data_len is <= 64 (RTN_BATCH_DL_LE64), which 64-byte slots
+        without ext need unless `out` has counters (include/retina_pc.h)."""
         import torch
 
         if n is None:
@@ -421,7 +448,7 @@ class PacketContinue:
         if out is None or out.n < n:
             out = self.alloc_outputs(n)
         b = _Batch(slab.data_ptr(), stride, data_len.data_ptr(), n, core_id,
-                   ext.data_ptr() if ext is not None else None)
+                   ext.data_ptr() if ext is not None else None, BATCH_DL_LE64 if dl_le64 else 0, 0)
         o = _out_struct(out)
         s = stream if stream is not None else torch.cuda.current_stream(self.device)
         _check(lib().rtn_pc_run(self._h, C.byref(b), C.byref(o), C.c_void_p(s.cuda_stream)))

@@ -69,6 +69,13 @@ def gpu_run(spec: str, slab: np.ndarray, stride: int, dlen: np.ndarray, device: 
     assert total == int(dl64.sum()), (total, int(dl64.sum()))
     assert ignored == int(dl64[~d["pc"][:n]].sum()) if n else ignored == 0
     l4 = d["l4"]
+    # TCP_PKT/BYTE, UDP_PKT/BYTE of process_packet (subscription/mod.rs:102-111), same launch
+    st = out.stats_host()
+    fidx = l4["pkt_idx"].astype(np.int64)
+    tcp = l4["proto"] == 6
+    assert (st["TCP_PKT"], st["UDP_PKT"]) == (int(tcp.sum()), int((~tcp).sum())), st
+    assert (st["TCP_BYTE"], st["UDP_BYTE"]) == (int(dl64[fidx[tcp]].sum()), int(dl64[fidx[~tcp]].sum())), st
+    assert cnt[3] == 0 or stride == 64, cnt
     rec = np.zeros(len(l4), REC)
     for f in ("ver", "proto", "flags", "sport", "dport", "offset", "length"):
         rec[f] = l4[f]

@@ -47,6 +47,8 @@ def _pred(rng: random.Random) -> str:
     if k == 11:
         return f"ipv4.total_length {rng.choice(['=', '<', '>'])} {rng.choice([0, 40, 50, 100])}"
     if k == 12:
+        if rng.random() < 0.5:  # an IP literal on a port field compiles (u32::from(u16), utils.rs:52-84)
+            return f"{rng.choice(['tcp', 'udp'])}.{rng.choice(['port', 'dst_port'])} {rng.choice(['=', '!='])} {rng.choice(['0.0.0.80', '0.0.0.53', '::50', '1.2.3.4'])}"
         return f"tcp.data_offset {rng.choice(['>', '='])} {rng.choice([5, 6])}"
     return rng.choice(L7)
 

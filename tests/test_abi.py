@@ -125,3 +125,69 @@ def test_rec_index_macro_matches_host_decoder(tmp_path):
         frames = np.arange(nch * 512)  # every slot of every chunk forwarded
         idx = pc._rec_index(frames, n)
         assert np.array_equal(np.sort(idx), np.arange(nch * 512))
+
+
+_RUST_C = {"u8": "uint8_t", "u16": "uint16_t", "u32": "uint32_t", "u64": "uint64_t", "i32": "int32_t",
+           "usize": "size_t"}
+_RUST_TO_HEADER = {"RtnBatch": "rtn_batch_t", "RtnPcOut": "rtn_pc_out_t", "RtnL4Ctx": "rtn_l4ctx_t",
+                   "RtnConn": "rtn_conn_t", "RtnProgramInfo": "rtn_program_info_t"}
+
+
+def _rust_structs(text: str) -> dict:
+    """`#[repr(C)] ... pub struct Name { pub field: type, ... }` blocks of INTEGRATION.md."""
+    import re
+
+    out = {}
+    for m in re.finditer(r"#\[repr\(C\)\][^\n]*\n?\s*pub struct (\w+)\s*\{(.*?)\}", text, re.S):
+        body = re.sub(r"//[^\n]*", "", m.group(2))
+        fields = re.findall(r"pub (\w+):\s*([^,]+?)\s*(?:,|$)", body, re.M)
+        if fields:
+            out[m.group(1)] = [(f, t.strip()) for f, t in fields]
+    return out
+
+
+def test_integration_rust_structs_match_header(tmp_path):
+    """The Rust #[repr(C)] structs documented in INTEGRATION.md §2 have the header's field order,
+    offsets and sizes: a C twin of each is compiled next to the header and compared with
+    _Static_assert (the documented binding had drifted)."""
+    import subprocess
+
+    text = (Path(__file__).resolve().parent.parent / "INTEGRATION.md").read_text()
+    structs = _rust_structs(text)
+    assert set(_RUST_TO_HEADER) <= set(structs), sorted(structs)
+    src = '#include "retina_pc.h"\n#include <stddef.h>\n#include <stdint.h>\n'
+    for name, cname in _RUST_TO_HEADER.items():
+        src += f"typedef struct {{\n"
+        for f, t in structs[name]:
+            src += f"  {'void*' if t.startswith('*') else _RUST_C[t]} {f};\n"
+        src += f"}} twin_{name};\n"
+        src += f"_Static_assert(sizeof(twin_{name}) == sizeof({cname}), \"size of {name}\");\n"
+        for f, _ in structs[name]:
+            src += (f"_Static_assert(offsetof(twin_{name}, {f}) == offsetof({cname}, {f}), \"{name}.{f}\");\n"
+                    f"_Static_assert(sizeof(((twin_{name}*)0)->{f}) == sizeof((({cname}*)0)->{f}), \"{name}.{f} size\");\n")
+    src += "int main(void) { return 0; }\n"
+    (tmp_path / "twin.c").write_text(src)
+    inc = Path(__file__).resolve().parent.parent / "include"
+    r = subprocess.run(["gcc", "-std=c11", "-Wall", "-Werror", f"-I{inc}", str(tmp_path / "twin.c"), "-o",
+                        str(tmp_path / "twin")], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    # every field of the C structs is in the twin (no field missing at the end either)
+    import re
+
+    hdr = (inc / "retina_pc.h").read_text()
+    for name, cname in _RUST_TO_HEADER.items():
+        body = re.search(r"typedef struct \w+ \{([^{}]*)\} " + cname + ";", hdr).group(1)
+        cfields = re.findall(r"^\s*[\w\s\*]+?\b(\w+);", re.sub(r"/\*.*?\*/", "", body, flags=re.S), re.M)
+        assert cfields == [f for f, _ in structs[name]], (name, cfields)
+
+
+def test_integration_extern_fns_exist():
+    """Every function the INTEGRATION.md bindings declare is declared by a header."""
+    import re
+
+    root = Path(__file__).resolve().parent.parent
+    text = (root / "INTEGRATION.md").read_text()
+    declared = set(re.findall(r"pub fn (rtn_\w+)\s*\(", text))
+    hdrs = "".join(h.read_text() for h in HEADERS)
+    missing = [f for f in declared if not re.search(r"\b" + f + r"\s*\(", hdrs)]
+    assert declared and not missing, missing

@@ -87,6 +87,41 @@ def test_narrow_stride_flags_status(gpu):
     assert got["counters"][3] & 1
 
 
+def test_slot_contract_is_never_silent(gpu):
+    """64-byte slots without ext (include/retina_pc.h): refused unless the caller asserts
+    RTN_BATCH_DL_LE64 or passes counters; an IPv6 frame with data_len > 64 is reported through
+    counters (RTN_STATUS_HDR_PAST_SLOT) or, without counters, through the context's sticky status
+    word (RTN_STATUS_DL_PAST_SLOT when the assertion was false); batches past RTN_MAX_FRAMES are
+    refused."""
+    import torch
+
+    ctx = pc.PacketContinue(pc.Program.from_spec(SETS["cfg2"]), 0)
+    frames = [helpers.build_frame(dport=80)] * 63 + [helpers.build_frame(True, 1, 2, payload=bytes(40))]
+    slab, dlen = pc.pack_frames(frames, 64)
+    assert dlen[-1] > 64 and dlen[:-1].max() <= 64
+    d_slab, d_dlen = torch.from_numpy(slab).cuda(), torch.from_numpy(dlen.view(np.int16)).cuda()
+    bare = ctx.alloc_outputs(64, counters=False)
+    with pytest.raises(pc.RetinaError) as e:
+        ctx.run(d_slab, 64, d_dlen, 64, bare)
+    assert e.value.code == -22 and "RTN_BATCH_DL_LE64" in str(e.value)
+    assert ctx.take_status() == 0
+    ctx.run(d_slab, 64, d_dlen, 64, bare, dl_le64=True)          # a false assertion ...
+    assert ctx.take_status() == pc.STATUS_DL_PAST_SLOT              # ... is reported, then cleared
+    assert ctx.take_status() == 0
+    ctx.run(d_slab, 64, d_dlen, 63, bare, dl_le64=True)          # a true one raises nothing
+    assert ctx.take_status() == 0
+    out = ctx.run(d_slab, 64, d_dlen, 64, ctx.alloc_outputs(64))  # counters: the caller sees it
+    torch.cuda.synchronize()
+    assert out.counters_host()[3] == pc.STATUS_HDR_PAST_SLOT
+    import dataclasses
+
+    huge = dataclasses.replace(bare, n=pc.MAX_FRAMES + 1)  # (refused before anything is touched)
+    with pytest.raises(pc.RetinaError) as e:
+        ctx.run(d_slab, 64, d_dlen, pc.MAX_FRAMES + 1, huge, dl_le64=True)
+    assert e.value.code == -22
+    assert ctx.take_status() == 0
+
+
 def test_full_size_cfg2_properties(gpu):
     """BASELINE config 2 at full size (2^25 frames): size-independent properties — the accept set
     is exactly dport == 80, every accepted frame is forwarded with offset 54 / length 10, records

@@ -205,3 +205,27 @@ def test_python_l4context_every_field_vs_c_oracle(name):
     assert len(recs) > 0
     if name in ("adversarial", "random", "synth"):
         assert n_v6 > 0
+
+
+@pytest.mark.parametrize("flt,port,want", [("tcp.dst_port = 0.0.0.80", 80, True), ("tcp.dst_port = 0.0.0.80", 81, False),
+                                           ("tcp.port = 1.2.3.4", 80, False), ("tcp.dst_port = ::50", 80, True),
+                                           ("udp.port != 0.0.0.53", 53, False)])
+def test_ip_literal_on_port_field_compiles(flt, port, want):
+    """binary_to_tokens (filtergen/src/utils.rs:52-121) emits `u32::from(tcp.dst_port()) == <addr>`
+    for an IPv4 literal on an integer field (u128::from for IPv6), which compiles in Rust
+    (From<u16> for u32/u128). Both compilers accept it and the comparison is on the port's value."""
+    import corpus as C
+
+    prod = pc.Program.from_filter(flt, ["ConnRecord"])
+    tree = filterlang.PacketTree([filterlang.Sub(flt, ["ConnRecord"])])
+    assert prod.tree == tree.pprint()
+    if flt.startswith("udp"):
+        u = C.udp(sport=port, dport=port)
+        f = C.eth(0x0800) + C.ipv4(17, len(u)) + u
+    else:
+        t = C.tcp(sport=1234, dport=port)
+        f = C.eth(0x0800) + C.ipv4(6, len(t)) + t
+    assert bool(packet.evaluate(tree, f)[0] & 1) is want
+    slab, dlen = pc.pack_frames([f], 128)
+    assert bool(helpers.oracle_run(prod_spec := synth._toml([(flt, ["ConnRecord"], "cb")]), slab, 128, dlen)["pc"][0]) is want
+    assert prod_spec

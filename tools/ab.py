@@ -1,0 +1,86 @@
+"""In-process A/B timing of kernel variants on one GPU (tools/README.md).
+
+    python tools/ab.py cfg2|cfg3|cfg4 VARIANT[:DEFINES][@GRID] ... [--reps R] [--frames N] [--mono]
+
+VARIANT names a tools/variants.py function (or several joined with '+'). Prints, per entry, the
+median kernel time over R interleaved rounds of 10 launches, Mpkt/s and the HBM-read roofline
+fraction of the bench's algorithmic bytes."""
+from __future__ import annotations
+
+import argparse
+import os
+import statistics
+import sys
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(ROOT / "tests"))
+sys.path.insert(0, str(ROOT / "tools"))
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("cfg")
+    ap.add_argument("entries", nargs="+")
+    ap.add_argument("--reps", type=int, default=7)
+    ap.add_argument("--frames", type=int, default=0)
+    ap.add_argument("--mono", action="store_true")
+    args = ap.parse_args()
+    import torch
+
+    import bench
+    import variants
+    from retina_amd import pc, synth
+
+    pc._LIB_PATH = pc._LIB_PATH.with_name("libretina_pc_exp.so")  # the experiments build
+    _, stride, n, _ = bench.CONFIGS[args.cfg]
+    n = args.frames or n
+    slab, dlen = bench.gen_frames(args.cfg, n, 0)
+    alg = synth.alg_read_bytes(slab, dlen, stride)
+    dev = torch.device("cuda", 0)
+    d_ext = None
+    if stride > 64 and not args.mono:
+        head, ext = pc.split_slab(slab, stride)
+        d_slab, d_ext = torch.from_numpy(head).to(dev), torch.from_numpy(ext).to(dev)
+        stride = 64
+    else:
+        d_slab = torch.from_numpy(slab).to(dev)
+    d_dlen = torch.from_numpy(dlen.view(np.int16)).to(dev)
+    le64 = stride == 64 and d_ext is None and int(dlen.max()) <= 64
+    spec = bench.spec_for(args.cfg)
+    tmp = ROOT / "gpurun_out" / "variants"
+    ctxs, out = [], None
+    for e in args.entries:
+        name, _, grid = e.partition("@")
+        name, _, defs = name.partition(":")
+        os.environ["RTN_KERNEL_TEMPLATE"] = str(variants.write(name, tmp))
+        os.environ["RTN_KERNEL_DEFINES"] = defs
+        ctx = pc.PacketContinue(pc.Program.from_spec(spec), 0)
+        if grid:
+            ctx.set_grid(int(grid))
+        out = out or ctx.alloc_outputs(n, addr6=True, counters=False)
+        ctxs.append((e, ctx))
+        print("compiled", e, flush=True)
+    times = {e: [] for e, _ in ctxs}
+    for _ in range(args.reps):
+        for e, ctx in ctxs:
+            for _ in range(2):
+                ctx.run(d_slab, stride, d_dlen, n, out, ext=d_ext, dl_le64=le64)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(10):
+                ctx.run(d_slab, stride, d_dlen, n, out, ext=d_ext, dl_le64=le64)
+            e1.record()
+            torch.cuda.synchronize()
+            times[e].append(e0.elapsed_time(e1) / 10)
+    for e, ts in times.items():
+        ms = statistics.median(ts)
+        print(f"{args.cfg} {e:40s} {ms:.4f} ms {n / ms / 1e3:9.1f} Mpkt/s frac {alg / ms / 1e6 / 8000:.3f} "
+              f"spread {(max(ts) - min(ts)) / ms:.3f}", flush=True)
+
+
+if __name__ == "__main__":
+    main()

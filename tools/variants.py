@@ -1,0 +1,60 @@
+"""Timing variants of retina_amd/csrc/kernels/pc_kernel.hip, made by text patches (tools/README.md).
+Each variant is a function src -> src; `base` is the product kernel unchanged."""
+from __future__ import annotations
+
+from pathlib import Path
+
+KERNEL = Path(__file__).resolve().parent.parent / "retina_amd" / "csrc" / "kernels" / "pc_kernel.hip"
+
+
+def _sub(src: str, old: str, new: str) -> str:
+    assert old in src, f"variant patch does not apply: {old[:60]!r}"
+    return src.replace(old, new)
+
+
+def base(src: str) -> str:
+    return src
+
+
+def ceiling(src: str) -> str:
+    """A fully coalesced 16-B-per-lane read of the head slab (+ ext for split): the HBM read
+    ceiling of the same bytes. Writes nothing."""
+    body = '''{
+  const rtn_u64 n16 = (rtn_u64)a.n * a.stride / 16u;
+  const rtn_v4u* p = reinterpret_cast<const rtn_v4u*>(a.slab);
+  rtn_u32 x = 0;
+  for (rtn_u64 k = blockIdx.x * (rtn_u64)blockDim.x + threadIdx.x; k < n16; k += (rtn_u64)gridDim.x * blockDim.x) {
+    const rtn_v4u v = __builtin_nontemporal_load(p + k);
+    x ^= v.x + v.y + v.z + v.w;
+  }
+  if (x == 0x9E3779B9u) a.counters[3] = x;
+}'''
+    for k in ("rtn_pc_kernel(rtn_args a) { rtn_run<RTN_MONO>(a); }",
+              "rtn_pc_kernel_s64(rtn_args a) { rtn_run<RTN_S64>(a); }",
+              "rtn_pc_kernel_split(rtn_args a) { rtn_run<RTN_SPLIT>(a); }"):
+        src = _sub(src, k, k.split(" {")[0] + " " + body)
+    return src
+
+
+def nostores(src: str) -> str:
+    """Everything but the record / IPv6-address / delivery stores (bitmaps still written)."""
+    src = _sub(src, "  if (fwd) {\n    const rtn_u32 r", "  if (fwd && a.n == 0u) {\n    const rtn_u32 r")
+    src = _sub(src, "    if (d) {", "    if (d && a.n == 0u) {")
+    src = _sub(src, "  const bool six = fwd && v.v6 && (a.flags & 1u);", "  const bool six = false;")
+    src = _sub(src, "    rtn_flush(a, ring, cring, ch, lane, ch.nrec - ch.nflushed);", "")
+    src = _sub(src, "  if (ch.nrec - ch.nflushed >= RTN_FLUSH) {", "  if (false) {")
+    return src
+
+
+VARIANTS = {"base": base, "ceiling": ceiling, "nostores": nostores}
+
+
+def write(name: str, outdir: Path) -> Path:
+    spec = name.split("+")
+    src = KERNEL.read_text()
+    for s in spec:
+        src = VARIANTS[s](src)
+    outdir.mkdir(parents=True, exist_ok=True)
+    p = outdir / f"pc_kernel_{name.replace('+', '_')}.hip"
+    p.write_text(src)
+    return p
