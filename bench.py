@@ -88,7 +88,12 @@ def cpu_baseline(cfg: str, slab: np.ndarray, dlen: np.ndarray, stride: int, runs
 
     lib = cgen.OracleLib(filterlang.PacketTree(filterlang.load_spec(spec_for(cfg))))
     BUF, HEAD, PER = 2176, 128, 1 << 18
+    # one pinned thread per CPU this process may use: the affinity mask, cut to the cgroup CPU
+    # quota when there is one (more threads than the quota only time-slice the same CPUs)
+    host = _host_cpus()
     cpus = sorted(os.sched_getaffinity(0))
+    if host["cgroup_quota_cpus"]:
+        cpus = cpus[:max(1, int(host["cgroup_quota_cpus"]))]
     res = {}
     for label, cl, target in (("1t", cpus[:1], target_1t), ("all", cpus, target_all)):
         # at most 8 GiB of mbufs in all: per thread 2^18, fewer on hosts with very many CPUs
@@ -121,14 +126,13 @@ def cpu_baseline(cfg: str, slab: np.ndarray, dlen: np.ndarray, stride: int, runs
                       "reps": reps, "seconds": secs, "pool": pool}
         del mem, view, ptrs
     a = res["all"]
-    host = _host_cpus()
     return {
         "value": round(a["mpps"], 2),
         "unit": "Mpkt/s",
         "cores": a["threads"],
         "kind": "port",
-        "sample": (f"{cfg} frames in 2176-B mbuf buffers (128-B headroom), {a['threads']} pinned threads (the whole "
-                   f"affinity mask) each cycling its own {a['pool'] // a['threads']} mbufs x {a['reps']} passes; median of {runs} runs "
+        "sample": (f"{cfg} frames in 2176-B mbuf buffers (128-B headroom), {a['threads']} pinned threads (every CPU "
+                   f"of the affinity mask within the cgroup quota) each cycling its own {a['pool'] // a['threads']} mbufs x {a['reps']} passes; median of {runs} runs "
                    f"({a['seconds']:.1f} s); 1 thread: {res['1t']['mpps']:.2f} Mpkt/s (median of {runs})"),
         "single_thread": round(res["1t"]["mpps"], 2),
         "runs_all": res["all"]["runs"],

@@ -574,8 +574,11 @@ __device__ __forceinline__ void rtn_run(const rtn_args& a) {
   constexpr bool stage6 = MODE != RTN_S64;  // 64-byte slots rarely forward IPv6 (only short UDP)
   __shared__ __attribute__((aligned(16))) rtn_v4u rtn_ring6[4][stage6 ? RTN_RING6 * 2u : 1u];
   rtn_v4u* ring6 = rtn_ring6[threadIdx.x >> 6];
-  __shared__ __attribute__((aligned(16))) rtn_u32 rtn_tile[4][slots64 ? 64 * RTN_XPITCH : 1];
+  // the transpose tile: 64-B head slots, and the bytes past 64 of the frames that need them
+  __shared__ __attribute__((aligned(16))) rtn_u32 rtn_tile[4][64 * RTN_XPITCH];
   rtn_u32* tile = rtn_tile[threadIdx.x >> 6];
+  __shared__ rtn_u32 rtn_ids[4][MODE != RTN_S64 ? 64 : 1];  // lanes that need bytes past 64, in order
+  rtn_u32* ids = rtn_ids[threadIdx.x >> 6];
   for (rtn_u32 c = wave_g; c < nchunks; c += nwaves) {
     const rtn_u32 gb = c * RTN_CHUNK_GROUPS;
     const rtn_u32 ge = gb + RTN_CHUNK_GROUPS < nw ? gb + RTN_CHUNK_GROUPS : nw;
@@ -597,15 +600,42 @@ __device__ __forceinline__ void rtn_run(const rtn_args& a) {
         for (int j = 0; j < 16; ++j) w[j] = lo[j];
 #pragma unroll
         for (int j = 16; j < 32; ++j) w[j] = 0u;
-        if (rtn_need_hi(lo, dl)) {
-          // bytes 64..127: the ext slot (split layout) or the slot's second half (monolithic)
-          const rtn_v4u* hi = MODE == RTN_SPLIT
-                                  ? reinterpret_cast<const rtn_v4u*>(a.ext + (rtn_u64)(g * 64u + lane) * 64u)
-                                  : reinterpret_cast<const rtn_v4u*>(a.slab + (rtn_u64)(g * 64u + lane) * a.stride) + 4;
+        // bytes 64..127 (the ext slot in the split layout, the slot's second half otherwise), only
+        // for the frames whose headers can pass byte 64: compacted, so that each full-width load
+        // brings the whole 64 B of 16 such frames (lane l: quarter l % 4 of the (l / 4)-th), and
+        // turned back into one row per owning lane through the LDS tile
+        const bool need = rtn_need_hi(lo, dl);
+        const rtn_u64 nm = __ballot(need);
+        if (nm) {
+          const rtn_u32 cnt = (rtn_u32)__popcll(nm);
+          if (need) ids[__popcll(nm & lane_lt)] = lane;
+          rtn_wave_sync();
+          rtn_v4u x[4];
+          rtn_u32 own[4];
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const rtn_v4u x = hi[j];
-            w[16 + 4 * j + 0] = x.x; w[16 + 4 * j + 1] = x.y; w[16 + 4 * j + 2] = x.z; w[16 + 4 * j + 3] = x.w;
+          for (rtn_u32 j = 0; j < 4u; ++j) {
+            const rtn_u32 k = 16u * j + (lane >> 2);
+            own[j] = ids[k < cnt ? k : 0u];
+            if (16u * j < cnt && k < cnt) {
+              const rtn_u64 f = (rtn_u64)g * 64u + own[j];
+              const rtn_v4u* hi = MODE == RTN_SPLIT ? reinterpret_cast<const rtn_v4u*>(a.ext + f * 64u)
+                                                    : reinterpret_cast<const rtn_v4u*>(a.slab + f * a.stride) + 4;
+              x[j] = hi[lane & 3u];
+            }
+          }
+#pragma unroll
+          for (rtn_u32 j = 0; j < 4u; ++j) {
+            const rtn_u32 k = 16u * j + (lane >> 2);
+            if (16u * j < cnt && k < cnt)
+              *reinterpret_cast<rtn_v4u*>(tile + own[j] * RTN_XPITCH + ((lane & 3u) ^ ((own[j] >> 2) & 3u)) * 4u) = x[j];
+          }
+          rtn_wave_sync();
+          if (need) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const rtn_v4u y = *reinterpret_cast<const rtn_v4u*>(tile + lane * RTN_XPITCH + ((j ^ (lane >> 2)) & 3u) * 4u);
+              w[16 + 4 * j + 0] = y.x; w[16 + 4 * j + 1] = y.y; w[16 + 4 * j + 2] = y.z; w[16 + 4 * j + 3] = y.w;
+            }
           }
         }
         rtn_group<32, stage6>(a, g, g - gb, lane, lane_lt, w, dl, ring, cring, ring6, ch, acc);

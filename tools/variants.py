@@ -49,12 +49,48 @@ def nostores(src: str) -> str:
 VARIANTS = {"base": base, "ceiling": ceiling, "nostores": nostores}
 
 
+def dense(src: str) -> str:
+    """Timing only: a chunk's records go to one dense 128-record region (chunk * 128 + k, no block
+    interleave; chunks with more than 128 records overlap their neighbours)."""
+    src = _sub(src, "rtn_v4u* dst = reinterpret_cast<rtn_v4u*>(a.recs + rtn_rec_slot(nch, ch.rec_base / (64u * RTN_CHUNK_GROUPS), ch.nflushed));",
+               "rtn_v4u* dst = reinterpret_cast<rtn_v4u*>(a.recs + ch.rec_base / 4u + ch.nflushed);")
+    return _sub(src, "if (k < nv4) RTN_ST(dst + (k / (RTN_RB * 3u / 2u)) * nch * (RTN_RB * 3u / 2u) + k % (RTN_RB * 3u / 2u), src[k]);",
+                "if (k < nv4) RTN_ST(dst + k, src[k]);")
+
+
+def nobitmaps(src: str) -> str:
+    """Timing only: no pc / fwd bitmap stores."""
+    src = _sub(src, "      RTN_ST8(a.pc_bm + gb + lane, ch.my_pc);\n", "")
+    return _sub(src, "      RTN_ST8(a.fwd_bm + gb + lane, ch.my_fwd);\n", "")
+
+
+def bm128(src: str) -> str:
+    """Timing only: the pc and fwd words of a chunk leave as one whole 128-B line (into the pc
+    bitmap, two chunks per line: overlapping)."""
+    src = _sub(src, "      RTN_ST8(a.pc_bm + gb + lane, ch.my_pc);\n      RTN_ST8(a.fwd_bm + gb + lane, ch.my_fwd);",
+               "      RTN_ST8(a.pc_bm + (gb & ~15u) + lane, ch.my_pc);\n    }\n    if (lane >= 8u && lane < 16u) {\n"
+               "      RTN_ST8(a.pc_bm + (gb & ~15u) + lane, __shfl(ch.my_fwd, (int)(lane - 8u)));")
+    return src
+
+
+def noext(src: str) -> str:
+    """Timing only: the bytes past 64 are never fetched (frames that need them parse zeros)."""
+    return _sub(src, "if (rtn_need_hi(lo, dl)) {", "if (rtn_need_hi(lo, dl) && a.n == 0u) {")
+
+
+VARIANTS.update({"dense": dense, "nobitmaps": nobitmaps, "bm128": bm128, "noext": noext})
+
+
 def write(name: str, outdir: Path) -> Path:
+    """A variant file: a '+'-joined list of VARIANTS applied to the current kernel, or
+    'file=<path>' (a kernel source as is, e.g. an older revision: git show REV:path > file)."""
+    outdir.mkdir(parents=True, exist_ok=True)
+    if name.startswith("file="):
+        return Path(name[5:]).resolve()
     spec = name.split("+")
     src = KERNEL.read_text()
     for s in spec:
         src = VARIANTS[s](src)
-    outdir.mkdir(parents=True, exist_ok=True)
     p = outdir / f"pc_kernel_{name.replace('+', '_')}.hip"
     p.write_text(src)
     return p
