@@ -141,6 +141,43 @@ def cpu_baseline(cfg: str, slab: np.ndarray, dlen: np.ndarray, stride: int, runs
     }
 
 
+def verify_sample(cfg: str, slab: np.ndarray, dlen: np.ndarray, stride: int, out, start: int) -> dict:
+    """Checker, outside the timed region: two 64K-frame windows of the run's own outputs against
+    the oracle (accept and forwarded bits, every L4Context field, IPv6 addresses, packet-level
+    callback masks). Raises on any difference, so a wrong kernel cannot print a bench line."""
+    import helpers
+
+    n = len(dlen)
+    d = out.decode()
+    l4 = d["l4"]
+    fi = l4["pkt_idx"].astype(np.int64)
+    win = min(1 << 16, n)
+    checked = []
+    for lo in sorted({(n // 3) & ~63, n - win}):
+        w = slice(lo, lo + win)
+        ora = helpers.oracle_run(spec_for(cfg), slab[lo * stride:(lo + win) * stride], stride, dlen[w])
+        sel = (fi >= lo) & (fi < lo + win)
+        got = {"pc": d["pc"][w], "fwd": d["fwd"][w], "rec": np.zeros(int(sel.sum()), helpers.REC),
+               "dm": np.zeros((win, ora["dm"].shape[1]), np.uint64)}
+        g = got["rec"]
+        for f in ("ver", "proto", "flags", "sport", "dport", "offset", "length"):
+            g[f] = l4[f][sel]
+        g["idx"], g["seq"], g["ack"] = l4["pkt_idx"][sel] - lo, l4["seq_no"][sel], l4["ack_no"][sel]
+        v4 = g["ver"] == 4
+        g["src"][v4, :4] = l4["src_ip4"][sel][v4].astype(">u4").view(np.uint8).reshape(-1, 4)
+        g["dst"][v4, :4] = l4["dst_ip4"][sel][v4].astype(">u4").view(np.uint8).reshape(-1, 4)
+        if "addr6" in d:
+            g["src"][~v4] = d["addr6"][sel][~v4, :16]
+            g["dst"][~v4] = d["addr6"][sel][~v4, 16:]
+        if "dlv" in d and ora["dm"].shape[1]:
+            rows = d["dlv"]
+            inw = (rows[:, 0] >= lo) & (rows[:, 0] < lo + win)
+            got["dm"][(rows[inw, 0] - lo).astype(np.int64)] = rows[inw, 1:1 + ora["dm"].shape[1]]
+        helpers.assert_same(got, ora, f"bench {cfg} frames [{lo}, {lo + win}) (+{start})")
+        checked.append([start + lo, win])
+    return {"windows": checked, "against": "oracle (generated C restatement)", "ok": True}
+
+
 def load_traffic(cfg: str, n: int):
     """Per-launch HBM bytes from the committed rocprofv3 PMC summary, if present."""
     p = ROOT / "profiles" / f"pmc_{cfg}.json"
@@ -403,6 +440,7 @@ def main() -> None:
     cnt_out = ctx.alloc_outputs(n, addr6=True, counters=True)
     ctx.run(d_slab, run_stride, d_dlen, n, cnt_out, stream=stream, ext=d_ext)
     torch.cuda.synchronize(dev)
+    verified = verify_sample(cfg, slab, dlen, stride, cnt_out, sh.start)
     counters = cnt_out.counters.view(torch.int32)[:3].to(torch.int64)
     stats = torch.tensor([wall, kern_ms], dtype=torch.float64, device=dev)
     rdist.reduce_totals(counters, stats)  # sum / max over ranks (RCCL), outside the timed region
@@ -441,6 +479,7 @@ def main() -> None:
                          "alg_bytes_per_frame": round(alg_bytes / n, 3)},
             "cpu_baseline": cpu,
             "accepted": {"packet_continue": counters[0], "forwarded": counters[1], "delivered": counters[2]},
+            "verified": verified,
             "e2e_pcie": e2e,
             "conn_stage": conn_stage,
         }

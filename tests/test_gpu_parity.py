@@ -158,6 +158,65 @@ def test_full_size_cfg2_properties(gpu):
     assert np.array_equal(l4["seq_no"][sel], ora["rec"]["seq"])
 
 
+@pytest.mark.parametrize("cfg,n", [("cfg3", 1 << 24), ("cfg4", 1 << 23)])
+def test_full_size_split_properties(cfg, n, gpu):
+    """BASELINE configs 3 and 4 at full size in the split layout the bench uses: the counters
+    equal the bitmaps' popcounts, the forwarded set is inside the accepted set, every record is a
+    well-formed L4Context (protocol, version, offset, UDP fields), the TCP/UDP byte counters equal
+    the data_len sums of the decoded records, and two 64K-frame windows (the start of the second
+    quarter and the last frames) equal the oracle exactly."""
+    import torch
+
+    import bench
+
+    slab, dlen = bench.gen_frames(cfg, n, 0)
+    spec = SETS[cfg]
+    head, ext = pc.split_slab(slab, 128)
+    ctx = pc.PacketContinue(pc.Program.from_spec(spec), 0)
+    dev = torch.device("cuda", 0)
+    out = ctx.run(torch.from_numpy(head).to(dev), 64, torch.from_numpy(dlen.view(np.int16)).to(dev), n,
+                  ext=torch.from_numpy(ext).to(dev))
+    del head, ext
+    torch.cuda.synchronize()
+    d = out.decode()
+    c = out.counters_host()
+    assert c[3] == 0
+    assert c[0] == d["pc"].sum() and c[1] == d["fwd"].sum() and not (d["fwd"] & ~d["pc"]).any()
+    dlv_frames = np.zeros(n, bool)
+    dlv_frames[d["dlv"][:, 0].astype(np.int64)] = True
+    assert c[2] == dlv_frames.sum() and (d["dlv"][:, 1:] != 0).any(1).all()
+    l4 = d["l4"]
+    v6 = l4["ver"] == 6
+    tcp = l4["proto"] == 6
+    assert set(np.unique(l4["proto"])) <= {6, 17} and set(np.unique(l4["ver"])) <= {4, 6}
+    assert (l4["offset"] % 4 == 2).all() and (l4["offset"] >= 14 + 20 + 8).all() and (l4["offset"] <= 22 + 60 + 60).all()
+    assert (l4["seq_no"][~tcp] == 0).all() and (l4["ack_no"][~tcp] == 0).all() and (l4["flags"][~tcp] == 0).all()
+    assert (d["addr6"][v6] != 0).any(1).all() and (l4["src_ip4"][v6] == 0).all()
+    st = out.stats_host()
+    dl = dlen.astype(np.int64)
+    fi = l4["pkt_idx"].astype(np.int64)
+    assert st["TCP_PKT"] == tcp.sum() and st["TCP_BYTE"] == dl[fi[tcp]].sum() and st["UDP_BYTE"] == dl[fi[~tcp]].sum()
+    assert st["TOTAL_BYTE"] == dl.sum() and st["IGNORED_BY_PACKET_FILTER_BYTE"] == dl[~d["pc"]].sum()
+    for lo in (n // 4, n - (1 << 16)):
+        w = slice(lo, lo + (1 << 16))
+        ora = helpers.oracle_run(spec, slab[lo * 128:(lo + (1 << 16)) * 128], 128, dlen[w])
+        assert np.array_equal(d["pc"][w], ora["pc"]) and np.array_equal(d["fwd"][w], ora["fwd"])
+        sel = (fi >= lo) & (fi < lo + (1 << 16))
+        got = l4[sel]
+        rec = ora["rec"]
+        assert np.array_equal(got["pkt_idx"] - lo, rec["idx"])
+        for gf, of in (("sport", "sport"), ("dport", "dport"), ("offset", "offset"), ("length", "length"),
+                       ("seq_no", "seq"), ("ack_no", "ack"), ("flags", "flags"), ("proto", "proto"), ("ver", "ver")):
+            assert np.array_equal(got[gf], rec[of]), (cfg, lo, gf)
+        gv4 = got["ver"] == 4
+        assert np.array_equal(got["src_ip4"][gv4].astype(">u4").view(np.uint8).reshape(-1, 4), rec["src"][gv4, :4])
+        assert np.array_equal(d["addr6"][sel][~gv4, :16], rec["src"][~gv4])
+        assert np.array_equal(d["addr6"][sel][~gv4, 16:], rec["dst"][~gv4])
+        dm = np.zeros((n, max(1, d["dlv"].shape[1] - 1)), np.uint64)
+        dm[d["dlv"][:, 0].astype(np.int64)] = d["dlv"][:, 1:]
+        assert np.array_equal(dm[w][:, :ora["dm"].shape[1]], ora["dm"])
+
+
 def test_large_tree_uses_nested_form_and_matches(gpu):
     """Trees past the straight-line threshold are emitted as nested if/else (codegen.cpp
     kFlatMaxNodes): 300 packet-level port subscriptions (a 600-node tree) plus packet-level

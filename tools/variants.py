@@ -75,7 +75,7 @@ def bm128(src: str) -> str:
 
 def noext(src: str) -> str:
     """Timing only: the bytes past 64 are never fetched (frames that need them parse zeros)."""
-    return _sub(src, "if (rtn_need_hi(lo, dl)) {", "if (rtn_need_hi(lo, dl) && a.n == 0u) {")
+    return _sub(src, "const bool need = rtn_need_hi(lo, dl);", "const bool need = rtn_need_hi(lo, dl) && a.n == 0u;")
 
 
 VARIANTS.update({"dense": dense, "nobitmaps": nobitmaps, "bm128": bm128, "noext": noext})
