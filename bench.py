@@ -56,6 +56,23 @@ def gen_frames(cfg: str, n: int, start: int, threads: int = 8):
     return slab, dlen
 
 
+def gen_rss_shard(cfg: str, n: int, rank: int, world: int, chunk: int = 1 << 21):
+    """This rank's frames of the global stream [0, world * n) under Retina's symmetric RSS
+    (retina_amd/dist.py rss_hash / rss_rank): the frames whose RETA queue is this rank's. The
+    count per rank varies with the hash; every rank reads the whole stream to find its own."""
+    from retina_amd import dist as rdist
+
+    stride = CONFIGS[cfg][1]
+    slabs, dls = [], []
+    for s0 in range(0, world * n, chunk):
+        k = min(chunk, world * n - s0)
+        sl, dl = gen_frames(cfg, k, start=s0)
+        keep = rdist.rss_rank(rdist.rss_hash(sl, stride, dl), world) == rank
+        slabs.append(sl.reshape(k, stride)[keep].reshape(-1))
+        dls.append(dl[keep])
+    return np.concatenate(slabs), np.concatenate(dls)
+
+
 def spec_for(cfg: str) -> str:
     from golden.filter_sets import SETS
 
@@ -314,6 +331,9 @@ def main() -> None:
     ap.add_argument("--no-conn", action="store_true", help="skip the connection-stage side measurement")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="N>1 collectives: nccl (= RCCL over xGMI) or gloo (CPU; rehearsal)")
+    ap.add_argument("--shard", choices=["contiguous", "rss"], default="contiguous",
+                    help="N>1: contiguous blocks of the frame stream per rank, or Retina's symmetric RSS "
+                         "hash (each connection on one rank; per-rank counts vary)")
     ap.add_argument("--layout", choices=["auto", "mono", "split"], default="auto",
                     help="slots wider than 64 B: monolithic, or split into 64-B head + 64-B ext slabs "
                          "(auto = split; include/retina_pc.h)")
@@ -328,7 +348,10 @@ def main() -> None:
     # one process per GPU; --dist-backend gloo with more ranks than GPUs rehearses the N>1 path
     # (barriers, max-over-ranks timing, totals reduction) on a single card
     gpu = local % max(1, torch.cuda.device_count())
-    if world > 1:
+    # launched by torch.distributed.run (N >= 1): one process group, RCCL by default, so the same
+    # barrier / max-over-ranks / all-reduce path runs at every N
+    distributed = world > 1 or "RANK" in os.environ
+    if distributed:
         torch.cuda.set_device(gpu)
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
@@ -342,9 +365,13 @@ def main() -> None:
 
     cfg = args.config
     _, stride, n_default, desc = CONFIGS[cfg]
-    n = args.frames or n_default
-    sh = rdist.shard(n, rank, world)  # weak scaling: a disjoint shard of the frame stream per rank
-    slab, dlen = gen_frames(cfg, sh.count, start=sh.start)
+    n_cfg = args.frames or n_default
+    sh = rdist.shard(n_cfg, rank, world)  # weak scaling: a disjoint shard of the frame stream per rank
+    if args.shard == "rss" and world > 1:
+        slab, dlen = gen_rss_shard(cfg, n_cfg, rank, world)
+    else:
+        slab, dlen = gen_frames(cfg, sh.count, start=sh.start)
+    n = len(dlen)  # this rank's frames
     alg_bytes = synth.alg_read_bytes(slab, dlen, stride)
     split = stride > 64 and args.layout != "mono"
     d_ext = None
@@ -370,7 +397,7 @@ def main() -> None:
     for _ in range(args.warmup):
         ctx.run(d_slab, run_stride, d_dlen, n, out, stream=stream, ext=d_ext, dl_le64=dl_le64)
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize(dev)
     ev0 = torch.cuda.Event(enable_timing=True)
@@ -381,7 +408,7 @@ def main() -> None:
         ctx.run(d_slab, run_stride, d_dlen, n, out, stream=stream, ext=d_ext, dl_le64=dl_le64)
     ev1.record(stream)
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
@@ -440,15 +467,17 @@ def main() -> None:
     cnt_out = ctx.alloc_outputs(n, addr6=True, counters=True)
     ctx.run(d_slab, run_stride, d_dlen, n, cnt_out, stream=stream, ext=d_ext)
     torch.cuda.synchronize(dev)
-    verified = verify_sample(cfg, slab, dlen, stride, cnt_out, sh.start)
-    counters = cnt_out.counters.view(torch.int32)[:3].to(torch.int64)
-    stats = torch.tensor([wall, kern_ms], dtype=torch.float64, device=dev)
+    verified = verify_sample(cfg, slab, dlen, stride, cnt_out, sh.start if args.shard == "contiguous" else 0)
+    counters = torch.cat([cnt_out.counters.view(torch.int32)[:3].to(torch.int64),
+                          torch.tensor([n], dtype=torch.int64, device=dev)])
+    stats = torch.tensor([wall, kern_ms, float(n)], dtype=torch.float64, device=dev)
     rdist.reduce_totals(counters, stats)  # sum / max over ranks (RCCL), outside the timed region
-    wall, kern_ms = float(stats[0]), float(stats[1])
+    wall, kern_ms, n_max = float(stats[0]), float(stats[1]), int(stats[2])
     counters = counters.cpu().tolist()
+    total_frames = counters[3]
 
     if rank == 0:
-        value = rdist.aggregate_mpps(n, world, args.steps, wall)
+        value = total_frames * args.steps / wall / 1e6  # every rank's frames over the slowest rank's time
         achieved = alg_bytes / (kern_ms / 1e3) / 1e9
         cpu = None
         if not args.no_cpu and world == 1:
@@ -472,7 +501,10 @@ def main() -> None:
             "config": {"workload": f"{cfg}: {desc}", "frames_per_gpu": n, "stride": stride,
                        "layout": "split (64-B head + 64-B ext slabs)" if split else f"{run_stride}-B slots",
                        "subscriptions": prog.info["n_subscriptions"], "tree_size": prog.info["tree_size"],
-                       "parallelism": f"shard{world}"},
+                       "parallelism": f"shard{world}",
+                       "shard": {"mode": args.shard if world > 1 else "none", "frames_total": total_frames,
+                                 "frames_max_rank": n_max,
+                                 "imbalance": round(n_max * world / total_frames, 4)}},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(cfg, n),
                          "alg_bytes_per_launch": alg_bytes, "kernel_ms": round(kern_ms, 4),
@@ -484,7 +516,7 @@ def main() -> None:
             "conn_stage": conn_stage,
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if distributed:
         dist.destroy_process_group()
 
 

@@ -371,10 +371,11 @@ __device__ __forceinline__ void rtn_flush(const rtn_args& a, const rtn_u64* ring
 
 // IPv6 address records (32 B: src, dst) are dense per chunk over the chunk's forwarded IPv6
 // frames. Where IPv6 is common (the split / wide-slot kernels) they leave through their own
-// per-wave LDS ring (128 entries, 4 KB) in whole 2-KB blocks: scattered 32-B stores with holes
-// between them cost about 4x their bytes in HBM time.
-#define RTN_RING6 128u
-#define RTN_FLUSH6 64u
+// per-wave LDS ring (64 entries, 2 KB) in whole 1-KB blocks: scattered 32-B stores with holes
+// between them cost about 4x their bytes in HBM time. (A 128-entry ring, 2-KB blocks, holds the
+// block to 3 per CU by LDS: cfg4 0.2028 -> 0.1942 ms with 64, in-process A/B.)
+#define RTN_RING6 64u
+#define RTN_FLUSH6 32u
 
 __device__ __forceinline__ void rtn_flush6(const rtn_args& a, const rtn_v4u* ring6, const rtn_chunk& ch, rtn_u32 lane,
                                            rtn_u32 nent) {
@@ -574,18 +575,29 @@ __device__ __forceinline__ void rtn_run(const rtn_args& a) {
   constexpr bool stage6 = MODE != RTN_S64;  // 64-byte slots rarely forward IPv6 (only short UDP)
   __shared__ __attribute__((aligned(16))) rtn_v4u rtn_ring6[4][stage6 ? RTN_RING6 * 2u : 1u];
   rtn_v4u* ring6 = rtn_ring6[threadIdx.x >> 6];
-  // the transpose tile: 64-B head slots, and the bytes past 64 of the frames that need them
-  __shared__ __attribute__((aligned(16))) rtn_u32 rtn_tile[4][64 * RTN_XPITCH];
+  __shared__ __attribute__((aligned(16))) rtn_u32 rtn_tile[4][slots64 ? 64 * RTN_XPITCH : 1];
   rtn_u32* tile = rtn_tile[threadIdx.x >> 6];
-  __shared__ rtn_u32 rtn_ids[4][MODE != RTN_S64 ? 64 : 1];  // lanes that need bytes past 64, in order
-  rtn_u32* ids = rtn_ids[threadIdx.x >> 6];
   for (rtn_u32 c = wave_g; c < nchunks; c += nwaves) {
     const rtn_u32 gb = c * RTN_CHUNK_GROUPS;
     const rtn_u32 ge = gb + RTN_CHUNK_GROUPS < nw ? gb + RTN_CHUNK_GROUPS : nw;
     rtn_chunk ch = {(rtn_u64)c * (64u * RTN_CHUNK_GROUPS), 0u, 0u, 0u, 0u, 0u, 0ull, 0ull, 0ull};
+    // 64-byte slots without ext: the next group's loads are issued before this group is parsed,
+    // so one group of loads is always in flight per wave (cfg2 -2.2 %, in-process A/B; with the
+    // split layout's dependent ext loads it measured 5 % slower on cfg4 and is not used there)
+    constexpr bool prefetch = MODE == RTN_S64;
+    rtn_v4u qn[4];
+    rtn_u32 dln = 0u;
+    if (prefetch) rtn_load_group(a, gb, lane, qn, dln);
     for (rtn_u32 g = gb; g < ge; ++g) {
       rtn_u32 lo[16], dl;
-      if (slots64) {
+      if (prefetch) {
+        rtn_v4u q[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) q[k] = qn[k];
+        dl = dln;
+        if (g + 1u < ge) rtn_load_group(a, g + 1u, lane, qn, dln);
+        rtn_xpose(tile, lane, q, lo);
+      } else if (slots64) {
         rtn_v4u q[4];
         rtn_load_group(a, g, lane, q, dl);
         rtn_xpose(tile, lane, q, lo);
@@ -600,42 +612,15 @@ __device__ __forceinline__ void rtn_run(const rtn_args& a) {
         for (int j = 0; j < 16; ++j) w[j] = lo[j];
 #pragma unroll
         for (int j = 16; j < 32; ++j) w[j] = 0u;
-        // bytes 64..127 (the ext slot in the split layout, the slot's second half otherwise), only
-        // for the frames whose headers can pass byte 64: compacted, so that each full-width load
-        // brings the whole 64 B of 16 such frames (lane l: quarter l % 4 of the (l / 4)-th), and
-        // turned back into one row per owning lane through the LDS tile
-        const bool need = rtn_need_hi(lo, dl);
-        const rtn_u64 nm = __ballot(need);
-        if (nm) {
-          const rtn_u32 cnt = (rtn_u32)__popcll(nm);
-          if (need) ids[__popcll(nm & lane_lt)] = lane;
-          rtn_wave_sync();
-          rtn_v4u x[4];
-          rtn_u32 own[4];
+        if (rtn_need_hi(lo, dl)) {
+          // bytes 64..127: the ext slot (split layout) or the slot's second half (monolithic)
+          const rtn_v4u* hi = MODE == RTN_SPLIT
+                                  ? reinterpret_cast<const rtn_v4u*>(a.ext + (rtn_u64)(g * 64u + lane) * 64u)
+                                  : reinterpret_cast<const rtn_v4u*>(a.slab + (rtn_u64)(g * 64u + lane) * a.stride) + 4;
 #pragma unroll
-          for (rtn_u32 j = 0; j < 4u; ++j) {
-            const rtn_u32 k = 16u * j + (lane >> 2);
-            own[j] = ids[k < cnt ? k : 0u];
-            if (16u * j < cnt && k < cnt) {
-              const rtn_u64 f = (rtn_u64)g * 64u + own[j];
-              const rtn_v4u* hi = MODE == RTN_SPLIT ? reinterpret_cast<const rtn_v4u*>(a.ext + f * 64u)
-                                                    : reinterpret_cast<const rtn_v4u*>(a.slab + f * a.stride) + 4;
-              x[j] = hi[lane & 3u];
-            }
-          }
-#pragma unroll
-          for (rtn_u32 j = 0; j < 4u; ++j) {
-            const rtn_u32 k = 16u * j + (lane >> 2);
-            if (16u * j < cnt && k < cnt)
-              *reinterpret_cast<rtn_v4u*>(tile + own[j] * RTN_XPITCH + ((lane & 3u) ^ ((own[j] >> 2) & 3u)) * 4u) = x[j];
-          }
-          rtn_wave_sync();
-          if (need) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              const rtn_v4u y = *reinterpret_cast<const rtn_v4u*>(tile + lane * RTN_XPITCH + ((j ^ (lane >> 2)) & 3u) * 4u);
-              w[16 + 4 * j + 0] = y.x; w[16 + 4 * j + 1] = y.y; w[16 + 4 * j + 2] = y.z; w[16 + 4 * j + 3] = y.w;
-            }
+          for (int j = 0; j < 4; ++j) {
+            const rtn_v4u x = hi[j];
+            w[16 + 4 * j + 0] = x.x; w[16 + 4 * j + 1] = x.y; w[16 + 4 * j + 2] = x.z; w[16 + 4 * j + 3] = x.w;
           }
         }
         rtn_group<32, stage6>(a, g, g - gb, lane, lane_lt, w, dl, ring, cring, ring6, ch, acc);

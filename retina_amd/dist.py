@@ -11,6 +11,8 @@ from __future__ import annotations
 import os
 from dataclasses import dataclass
 
+import numpy as np
+
 
 @dataclass(frozen=True)
 class Shard:
@@ -32,12 +34,79 @@ def shard(frames_per_rank: int, rank: int, world: int) -> Shard:
     return Shard(rank, world, rank * frames_per_rank, frames_per_rank)
 
 
+# Retina's symmetric RSS key (core/src/port/mod.rs:22-28) and redirection table size (:28, 156-165)
+SYMMETRIC_RSS_KEY = bytes([0x6D, 0x5A] * 26)
+RSS_RETA_SIZE = 512
+
+
+def _toeplitz_tables(key: bytes = SYMMETRIC_RSS_KEY, nbytes: int = 36) -> np.ndarray:
+    """T[p][v] = the Toeplitz hash contribution of byte value v at input byte p: the XOR of the
+    32-bit key windows starting at every set bit of v (bit 7 of byte 0 first)."""
+    kbits = int.from_bytes(key, "big")
+    klen = 8 * len(key)
+    win = np.array([(kbits >> (klen - 32 - i)) & 0xFFFFFFFF for i in range(8 * nbytes)], np.uint64)
+    t = np.zeros((nbytes, 256), np.uint64)
+    for p in range(nbytes):
+        for b in range(8):
+            on = (np.arange(256) >> (7 - b)) & 1
+            t[p] ^= np.where(on == 1, win[8 * p + b], 0).astype(np.uint64)
+    return t.astype(np.uint32)
+
+
+_TT = None
+
+
+def rss_hash(slab: np.ndarray, stride: int, dlen: np.ndarray) -> np.ndarray:
+    """The NIC's RSS hash of each frame under Retina's port configuration
+    (core/src/port/mod.rs:320-331: rss_hf = ETH_RSS_IP | ETH_RSS_TCP | ETH_RSS_UDP, symmetric
+    key): Toeplitz over src addr | dst addr [| src port | dst port] for IPv4 / IPv6 with TCP or
+    UDP, over the addresses only for other IP frames, 0 for non-IP frames. The headers are located
+    with the packet parsers' rules (Ethernet / one 802.1Q tag / IPv4 IHL / IPv6 without extension
+    headers). With the symmetric key both directions of a connection hash alike, so a connection's
+    frames all land on one rank."""
+    global _TT
+    if _TT is None:
+        _TT = _toeplitz_tables()
+    b = np.ascontiguousarray(slab, np.uint8).reshape(-1, stride)
+    n = len(dlen)
+    rows = np.arange(n)
+    et = (b[:, 12].astype(np.int64) << 8) | b[:, 13]
+    vl = et == 0x8100
+    l3 = np.where(vl, 18, 14)
+    inner = np.where(vl, (b[:, 16].astype(np.int64) << 8) | b[:, 17], et)
+    dl = dlen.astype(np.int64)
+    v4 = (inner == 0x0800) & (l3 + 20 <= dl)
+    v6 = (inner == 0x86DD) & (l3 + 40 <= dl)
+    col = lambda off: b[rows, np.minimum(off, stride - 1)]  # noqa: E731
+    proto = np.where(v4, col(l3 + 9), col(l3 + 6)).astype(np.int64)
+    l4 = l3 + np.where(v4, (col(l3) & 15).astype(np.int64) * 4, 40)
+    ports = (v4 | v6) & ((proto == 6) | (proto == 17)) & (l4 + 4 <= np.minimum(dl, stride))
+    h = np.zeros(n, np.uint32)
+    # IPv4: src(4) dst(4) [sport dport]; IPv6: src(16) dst(16) [ports]
+    for p in range(8):
+        h ^= np.where(v4, _TT[p][col(l3 + 12 + p)], 0).astype(np.uint32)
+    for p in range(4):
+        h ^= np.where(v4 & ports, _TT[8 + p][col(l4 + p)], 0).astype(np.uint32)
+    for p in range(32):
+        h ^= np.where(v6, _TT[p][col(l3 + 8 + p)], 0).astype(np.uint32)
+    for p in range(4):
+        h ^= np.where(v6 & ports, _TT[32 + p][col(l4 + p)], 0).astype(np.uint32)
+    return h
+
+
+def rss_rank(hashes: np.ndarray, world: int) -> np.ndarray:
+    """Queue / GPU of each frame: RETA[hash % 512] with the RETA filled round-robin over the
+    queues (port/mod.rs:156-165), one queue per rank."""
+    return ((hashes.astype(np.int64) % RSS_RETA_SIZE) % world).astype(np.int64)
+
+
 def reduce_totals(totals, times):
     """Sum the per-rank totals (int64 tensor) and take the max of the per-rank times (float64
-    tensor) over all ranks, in place; a no-op on one rank. Returns (totals, times)."""
+    tensor) over all ranks, in place, whenever a process group is up (one rank included, so the
+    RCCL path runs even at N=1 under torch.distributed.run). Returns (totals, times)."""
     import torch.distributed as dist
 
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+    if dist.is_available() and dist.is_initialized():
         host = dist.get_backend() == "gloo" and totals.is_cuda  # gloo reduces host tensors
         t, m = (totals.cpu(), times.cpu()) if host else (totals, times)
         dist.all_reduce(t, op=dist.ReduceOp.SUM)

@@ -85,3 +85,100 @@ def test_shard_bounds():
     assert (s.start, s.count) == (300, 100)
     with pytest.raises(ValueError):
         rdist.shard(100, 4, 4)
+
+
+def test_toeplitz_known_answers_and_symmetry():
+    """retina_amd.dist's Toeplitz hash reproduces the published RSS verification vectors (the
+    Microsoft RSS key, IPv4 with ports) and, under Retina's symmetric key
+    (core/src/port/mod.rs:22-28), hashes both directions of a connection alike."""
+    import ipaddress
+
+    import helpers
+    from retina_amd import dist as rdist
+    from retina_amd import pc
+
+    ms_key = bytes.fromhex("6d5a56da255b0ec24167253d43a38fb0d0ca2bcbae7b30b477cb2da38030f20c6a42b73bbeac01fa")
+    t = rdist._toeplitz_tables(ms_key, 12)
+    for src, dst, sp, dp, want in (("66.9.149.187", "161.142.100.80", 2794, 1766, 0x51CCC178),
+                                   ("199.92.111.2", "65.69.140.83", 14230, 4739, 0xC626B0EA),
+                                   ("24.19.198.95", "12.22.207.184", 12898, 38024, 0x5C2B394A)):
+        inp = ipaddress.IPv4Address(src).packed + ipaddress.IPv4Address(dst).packed + sp.to_bytes(2, "big") + dp.to_bytes(2, "big")
+        h = 0
+        for p, v in enumerate(inp):
+            h ^= int(t[p][v])
+        assert h == want
+    rng = np.random.default_rng(3)
+    frames = []
+    for _ in range(300):
+        v6 = bool(rng.random() < 0.3)
+        a, b = int(rng.integers(0, 1 << 32)), int(rng.integers(0, 1 << 32))
+        pa, pb = int(rng.integers(1, 65536)), int(rng.integers(1, 65536))
+        pr = 6 if rng.random() < 0.5 else 17
+        frames += [helpers.build_frame(v6, a, b, pa, pb, pr, 0x02), helpers.build_frame(v6, b, a, pb, pa, pr, 0x12)]
+    slab, dlen = pc.pack_frames(frames, 128)
+    h = rdist.rss_hash(slab, 128, dlen)
+    assert (h[0::2] == h[1::2]).all() and len(set(h.tolist())) > 290
+    ranks = rdist.rss_rank(h, 8)
+    assert set(ranks.tolist()) == set(range(8))
+
+
+def test_rss_shards_partition_the_stream():
+    """bench.py --shard rss: the ranks' frames partition the global stream (every frame on exactly
+    one rank, frame order kept) and the per-rank counts are near even."""
+    import bench
+    from retina_amd import dist as rdist
+
+    n, world = 1 << 14, 4
+    full, fd = bench.gen_frames("cfg3", world * n, 0)
+    parts = [bench.gen_rss_shard("cfg3", n, r, world) for r in range(world)]
+    assert sum(len(d) for _, d in parts) == world * n
+    rk = rdist.rss_rank(rdist.rss_hash(full, 128, fd), world)
+    for r, (s, d) in enumerate(parts):
+        assert np.array_equal(d, fd[rk == r])
+        assert np.array_equal(s.reshape(-1, 128), full.reshape(-1, 128)[rk == r])
+        assert abs(len(d) - n) < n * 0.1
+
+
+@pytest.mark.gpu
+def test_rccl_process_group_one_rank(gpu):
+    """The RCCL path bench.py takes under torch.distributed.run: a 1-rank "nccl" process group bound
+    to cuda:0, the totals / times reduction on device tensors (reduce_totals), and a barrier."""
+    import torch
+    import torch.distributed as dist
+
+    from retina_amd import dist as rdist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        tot = torch.tensor([5, 7, 11], dtype=torch.int64, device="cuda")
+        tim = torch.tensor([0.25, 1.5], dtype=torch.float64, device="cuda")
+        rdist.reduce_totals(tot, tim)
+        dist.barrier()
+        torch.cuda.synchronize()
+        assert tot.tolist() == [5, 7, 11] and tim.tolist() == [0.25, 1.5]
+        assert dist.get_backend() == "nccl"
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shard", ["contiguous", "rss"])
+def test_bench_under_torchrun_rccl(gpu, shard, tmp_path):
+    """bench.py as the driver launches it for N GPUs (python -m torch.distributed.run ... bench.py
+    --gpus N), here N = 1 on one card with RCCL: it prints one JSON line with the reduced totals."""
+    import json
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parent.parent
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1", "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port()), str(root / "bench.py"), "--gpus", "1", "--steps", "3",
+           "--warmup", "1", "--frames", str(1 << 20), "--no-cpu", "--no-e2e", "--no-conn", "--shard", shard]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=root)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == 1 and line["value"] > 0 and line["verified"]["ok"]
+    assert line["config"]["shard"]["frames_total"] == 1 << 20
