@@ -149,7 +149,8 @@ typedef struct rtn_pc_out {
   rtn_l4ctx_t* l4;       /* [ceil(n/512)*512] (rtn_out_l4_bytes) at RTN_REC_INDEX; unused slots undefined */
   uint8_t* addr6;        /* optional [ceil(n/512)*512][32]: src|dst of the IPv6 records   */
   uint64_t* dlv_bitmap;  /* [ceil(n/64)] frames with >= 1 packet-level callback (if any)     */
-  uint64_t* dlv_records; /* [ceil(n/512)*512][1 + deliver_words]: frame index, statement mask */
+  uint64_t* dlv_records; /* [ceil(n/512)*512][deliver_words]: statement mask; the frame is the
+                          record's rank among its chunk's dlv_bitmap bits (as for l4)        */
   uint32_t* counters;    /* optional [16] (RTN_COUNTERS_BYTES = 64 B, 8-B aligned), zeroed per run
                           (NULL: no totals, no memset -- one kernel launch); RTN_CNT_* below */
   rtn_conn_t* conn;      /* optional [ceil(n/512)*512]: connection stage, indexed like l4       */

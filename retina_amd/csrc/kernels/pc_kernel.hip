@@ -67,7 +67,7 @@ struct rtn_args {
   rtn_l4rec* recs;            // [ceil(n/512)*512], dense per chunk
   unsigned char* addr6;       // [ceil(n/64)*64][32] (src, dst) raw bytes, IPv6 records only
   rtn_u64* dlv_bm;            // [ceil(n/64)]  any packet-level delivery
-  rtn_u64* dlv_recs;          // [ceil(n/64)*64][1 + RTN_DELIVER_WORDS]  (pkt_idx, statement mask words)
+  rtn_u64* dlv_recs;          // [ceil(n/512)*512][RTN_DELIVER_WORDS] statement masks, ranked by dlv_bm per chunk
   rtn_u32* counters;          // [0] pc, [1] fwd, [2] dlv, [3] status, [4..5] bytes, [6..7] ignored bytes,
                               // [8] tcp, [9] udp (forwarded), [10..11] tcp bytes, [12..13] udp bytes
   const unsigned char* ext;   // split layout: bytes 64..127 of each frame (64-byte slots), or null
@@ -542,10 +542,10 @@ __device__ __forceinline__ void rtn_group(const rtn_args& a, rtn_u32 g, rtn_u32 
     acc.dlv += (rtn_u32)__popcll(dlvm);
     if (d) {
       const rtn_u64 slot_i = ch.rec_base + ch.ndlv + (rtn_u32)__popcll(dlvm & lane_lt);
-      rtn_u64* dp = a.dlv_recs + slot_i * (1u + RTN_DELIVER_WORDS);
-      RTN_ST8(dp, (rtn_u64)i);
+      // the frame index is implied by the record's rank in dlv_bm (like the L4Context records)
+      rtn_u64* dp = a.dlv_recs + slot_i * RTN_DELIVER_WORDS;
 #pragma unroll
-      for (int j = 0; j < RTN_DELIVER_WORDS; ++j) RTN_ST8(dp + 1 + j, dm[j]);
+      for (int j = 0; j < RTN_DELIVER_WORDS; ++j) RTN_ST8(dp + j, dm[j]);
     }
     ch.ndlv += (rtn_u32)__popcll(dlvm);
   }

@@ -606,7 +606,7 @@ static_assert(sizeof(rtn_l4ctx_t) == 24, "rtn_l4ctx_t is 24 bytes");
 size_t rtn_out_l4_bytes(uint32_t n) { return chunked(n) * sizeof(rtn_l4ctx_t); }
 size_t rtn_out_addr6_bytes(uint32_t n) { return chunked(n) * 32u; }
 size_t rtn_out_dlv_bytes(uint32_t n, uint32_t deliver_words) {
-  return chunked(n) * (1u + deliver_words) * 8u;
+  return chunked(n) * (size_t)deliver_words * 8u;
 }
 static_assert(sizeof(rtn_conn_t) == 8, "rtn_conn_t is 8 bytes");
 size_t rtn_out_conn_bytes(uint32_t n) { return chunked(n) * sizeof(rtn_conn_t); }

@@ -340,9 +340,11 @@ class PCOutputs:
                 out["conn_dlv"] = cd[idx]
         if self.deliver_words:
             dbm = self.dlv_bitmap.cpu().numpy().view(np.uint64)
-            recs_d = self.dlv_records.cpu().numpy().view(np.uint64).reshape(-1, 1 + self.deliver_words)
+            recs_d = self.dlv_records.cpu().numpy().view(np.uint64).reshape(-1, self.deliver_words)
             di = _segment_index(dbm)
-            out["dlv"] = recs_d[di]
+            # rows of (frame index, statement mask words): the index is the bit's position
+            frames = np.nonzero(np.unpackbits(dbm.view(np.uint8), bitorder="little")[:n])[0].astype(np.uint64)
+            out["dlv"] = np.column_stack([frames, recs_d[di]]) if len(frames) else np.zeros((0, 1 + self.deliver_words), np.uint64)
         return out
 
 

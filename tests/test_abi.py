@@ -71,7 +71,9 @@ def test_output_sizes():
     assert L.rtn_out_l4_bytes(65) == 512 * 24
     assert L.rtn_out_l4_bytes(1025) == 1536 * 24
     assert L.rtn_out_addr6_bytes(1) == 512 * 32
-    assert L.rtn_out_dlv_bytes(64, 2) == 512 * 3 * 8
+    assert L.rtn_out_dlv_bytes(64, 2) == 512 * 2 * 8      # masks only: the frame is the rank in dlv_bitmap
+    assert L.rtn_out_bitmap_bytes(0xFFFFFFFF) == ((1 << 32) // 64) * 8   # 64-bit arithmetic, no wrap
+    assert L.rtn_out_l4_bytes(0xFFFFFFFF) == (1 << 32) * 24
 
 
 def test_headers_are_c(tmp_path):
