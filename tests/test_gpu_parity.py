@@ -189,8 +189,8 @@ def test_full_size_split_properties(cfg, n, gpu):
     v6 = l4["ver"] == 6
     tcp = l4["proto"] == 6
     assert set(np.unique(l4["proto"])) <= {6, 17} and set(np.unique(l4["ver"])) <= {4, 6}
-    # IHL and doff are not sanity-checked (ipv4.rs:215-217, tcp.rs:222-224): 14 + 0 + 8 .. 22 + 60 + 60
-    assert (l4["offset"] % 4 == 2).all() and (l4["offset"] >= 14 + 8).all() and (l4["offset"] <= 22 + 60 + 60).all()
+    # IHL and doff are not sanity-checked (ipv4.rs:215-217, tcp.rs:222-224): 14 + 0 + 0 .. 22 + 60 + 60
+    assert (l4["offset"] % 4 == 2).all() and (l4["offset"] >= 14).all() and (l4["offset"] <= 22 + 60 + 60).all()
     assert (l4["seq_no"][~tcp] == 0).all() and (l4["ack_no"][~tcp] == 0).all() and (l4["flags"][~tcp] == 0).all()
     assert (d["addr6"][v6] != 0).any(1).all() and (l4["src_ip4"][v6] == 0).all()
     st = out.stats_host()
