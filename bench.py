@@ -29,6 +29,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 CONFIGS = {
     # name: (generator, stride, frames per GPU, description)
+    "cfg1": ("traces", 128, 1 << 20, "the reference's traces/*.pcap frames (small_flows.pcap is absent), tiled; "
+                                      "examples/basic (tls, dns)"),
     "cfg2": ("cfg2", 64, 1 << 25, "64 B synthetic Eth/IPv4/TCP, tcp.dst_port = 80 (ConnRecord), 2^25 frames/GPU"),
     "cfg3": ("cfg3", 128, 1 << 24, "IMIX 64/594/1518 + VLAN/IPv6/malformed, 6 subscriptions (examples/protocols + filter_stats)"),
     "cfg4": ("cfg4", 128, 1 << 23, "1500 B IPv4/IPv6 x TCP/UDP, 42 subscriptions (64 distinct predicates)"),
@@ -38,8 +40,15 @@ CONFIGS = {
 def gen_frames(cfg: str, n: int, start: int, threads: int = 8):
     from retina_amd import synth
 
-    fn = getattr(synth, CONFIGS[cfg][0])
     stride = CONFIGS[cfg][1]
+    if CONFIGS[cfg][0] == "traces":
+        # config 1: the 1287 frames of the reference's traces (tests/golden/traces.npz, made from
+        # traces/*.pcap by tests/golden/make_golden.py as offline.rs hands them over), repeated
+        t = np.load(ROOT / "tests" / "golden" / "traces.npz")
+        k = len(t["dlen"])
+        idx = (np.arange(n, dtype=np.int64) + start) % k
+        return np.ascontiguousarray(t["slab"].reshape(k, stride)[idx]).reshape(-1), t["dlen"][idx].copy()
+    fn = getattr(synth, CONFIGS[cfg][0])
     chunk = 1 << 21
     starts = list(range(0, n, chunk))
     slab = np.empty(n * stride, np.uint8)
@@ -76,7 +85,7 @@ def gen_rss_shard(cfg: str, n: int, rank: int, world: int, chunk: int = 1 << 21)
 def spec_for(cfg: str) -> str:
     from golden.filter_sets import SETS
 
-    return SETS[cfg]
+    return SETS["basic" if cfg == "cfg1" else cfg]
 
 
 def _host_cpus() -> dict:

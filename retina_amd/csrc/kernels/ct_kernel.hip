@@ -250,10 +250,16 @@ extern "C" __global__ void __launch_bounds__(RTN_CT_BLOCK) rtn_ct_insert(rtn_ct_
 #pragma unroll
   for (rtn_u32 u = 0; u < G; ++u)
     if (active[u]) rtn_ct_make_key(a, f.rec[u], f.cv[u], f.a6[u], k[u]);
-  // Phase A: find the key or the first empty slot of its probe chain (no writes).
+  // Phase A: find the key or the first empty slot of its probe chain (no writes), remembering the
+  // chain's first removed slot: a key known to be absent reuses it, so that removals do not
+  // leave the chains to fill up with tombstones until a rebuild.
   bool at_empty[G];
+  rtn_u32 tomb[G];
 #pragma unroll
-  for (rtn_u32 u = 0; u < G; ++u) at_empty[u] = false;
+  for (rtn_u32 u = 0; u < G; ++u) {
+    at_empty[u] = false;
+    tomb[u] = 0xffffffffu;
+  }
   for (rtn_u32 p = 0; p < RTN_CT_MAXPROBE; ++p) {
     bool more = false;
 #pragma unroll
@@ -271,6 +277,7 @@ extern "C" __global__ void __launch_bounds__(RTN_CT_BLOCK) rtn_ct_insert(rtn_ct_
         } else if (t == RTN_CT_EMPTY) {
           at_empty[u] = true;
         } else {
+          if (t == RTN_CT_REMOVED && tomb[u] == 0xffffffffu) tomb[u] = slot[u];
           slot[u] = (slot[u] + 1u) & a.cap_mask;
           more = true;
         }
@@ -282,6 +289,7 @@ extern "C" __global__ void __launch_bounds__(RTN_CT_BLOCK) rtn_ct_insert(rtn_ct_
 #pragma unroll
   for (rtn_u32 u = 0; u < G; ++u) {
     active[u] = active[u] && at_empty[u];  // probe limit reached without an empty slot: full
+    if (active[u] && tomb[u] != 0xffffffffu) slot[u] = tomb[u];  // claim from the first removed slot
     want += (rtn_u32)__popcll(__ballot(active[u]));
   }
   // Admission (ConnTracker's size < max_connections): the block reserves one ticket per opener
@@ -304,7 +312,9 @@ extern "C" __global__ void __launch_bounds__(RTN_CT_BLOCK) rtn_ct_insert(rtn_ct_
       if (active[u] && ticket >= blk[2]) active[u] = false;  // table full for this opener
     }
   }
-  // Phase B: claim from the empty slot on (another lane may take it first: keep probing).
+  // Phase B: claim from the first free (empty or removed) slot on (another lane may take it
+  // first: keep probing). A removed slot was reset to epoch 0 / first 0xffffffff by its removal,
+  // so until its claimer has written the epoch, lanes of the same key lower `first` (phase A).
   rtn_u32 claims = 0u;
   for (rtn_u32 p = 0; p < RTN_CT_MAXPROBE; ++p) {
     bool more = false;
@@ -313,8 +323,9 @@ extern "C" __global__ void __launch_bounds__(RTN_CT_BLOCK) rtn_ct_insert(rtn_ct_
       if (active[u]) {
         rtn_u64* tag = rtn_ct_tag(a, slot[u]);
         rtn_u64 t = __hip_atomic_load(tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (t == RTN_CT_EMPTY) t = atomicCAS(tag, RTN_CT_EMPTY, k[u].fp);
-        if (t == RTN_CT_EMPTY) {
+        const rtn_u64 seen = t;
+        if (t <= RTN_CT_REMOVED) t = atomicCAS(tag, seen, k[u].fp);
+        if (t == seen && seen <= RTN_CT_REMOVED) {
           atomicOr(&a.occ[slot[u] >> 5], 1u << (slot[u] & 31u));
           rtn_u32* s = a.table + (rtn_u64)slot[u] * 16u;
           s[2] = a.epoch;
@@ -365,17 +376,10 @@ extern "C" __global__ void __launch_bounds__(RTN_CT_BLOCK) rtn_ct_lookup(rtn_ct_
   // Every group's first probe is issued before any is used: the start slot's occupancy bit (in
   // L2; most misses end here), then the tags of occupied start slots, then the slots whose tag
   // matches. Only chains (start slot held by another key or removed) probe further, one by one.
-  bool occ0[G], occx[G] = {};
+  bool occ0[G];
 #pragma unroll
   for (rtn_u32 u = 0; u < G; ++u) {
-#if defined(RTN_CT_EXP_NO_PROBE)
-    occ0[u] = false;  // experiment: loads, status and store only
-#elif defined(RTN_CT_EXP_OCC_ONLY)
-    occ0[u] = false;  // experiment: the occupancy reads only (kept alive in the store)
-    occx[u] = f.has[u] && rtn_ct_occupied(a.occ, (rtn_u32)f.cv[u] & a.cap_mask);
-#else
     occ0[u] = f.has[u] && rtn_ct_occupied(a.occ, (rtn_u32)f.cv[u] & a.cap_mask);
-#endif
   }
   // an occupied start slot is read whole (tag, epoch, first, key: one 64-B line) in one go
   rtn_ct_key k[G];
@@ -443,7 +447,6 @@ extern "C" __global__ void __launch_bounds__(RTN_CT_BLOCK) rtn_ct_lookup(rtn_ct_
     }
     if (status == 0u) status = !opens ? RTN_CT_MISS : dropped ? RTN_CT_NEW_DROPPED : RTN_CT_FULL;
     if (status == RTN_CT_COLLISION) found = 0xffffffffu;
-    if (occx[u]) status |= 0x80000000u;
     __builtin_nontemporal_store((rtn_u64)found | ((rtn_u64)status << 32), a.out + f.r[u]);
   }
 }
@@ -456,6 +459,10 @@ extern "C" __global__ void __launch_bounds__(256) rtn_ct_remove_k(rtn_u32* table
   rtn_u64* tag = reinterpret_cast<rtn_u64*>(table + (rtn_u64)slot * 16u);
   const rtn_u64 t = *tag;
   if (t > RTN_CT_REMOVED) {
+    // a tombstone: lookups walk past it, an insert reuses it (epoch 0 and first 0xffffffff: the
+    // state of a slot whose claimer has not written it yet)
+    table[(rtn_u64)slot * 16u + 2u] = 0u;
+    table[(rtn_u64)slot * 16u + 3u] = 0xffffffffu;
     *tag = RTN_CT_REMOVED;
     atomicSub(&live[0], 1u);
   }

@@ -63,8 +63,8 @@ def main(tag: str, cfg: str, frames: int) -> None:
     fetch = counter(out / f"pmc_{tag}_{cfg}_1" / "run_counter_collection.csv", "FETCH_SIZE")
     write = counter(out / f"pmc_{tag}_{cfg}_2" / "run_counter_collection.csv", "WRITE_SIZE")
     extra = {}
-    for k in (3, 4):
-        p = out / f"pmc_{tag}_{cfg}_{k}" / "run_counter_collection.csv"
+    for ps in (3, 4):
+        p = out / f"pmc_{tag}_{cfg}_{ps}" / "run_counter_collection.csv"
         if p.exists():
             extra.update(counters(p))
     f_kb, w_kb = statistics.median(fetch), statistics.median(write)

@@ -194,3 +194,28 @@ def test_ct_large_batch_properties(gpu):
     assert (s2[s1 == pc.CT_MISS] == pc.CT_MISS).all()
     assert (s2[s1 == pc.CT_NEW_DROPPED] == pc.CT_NEW_DROPPED).all()
     assert ct.stats()["live"] == int(new.sum())
+
+
+@pytest.mark.gpu
+def test_ct_churn_reuses_removed_slots(gpu):
+    """Connections opened and removed batch after batch, 4x the table's capacity in all: removed
+    slots are reused, so no opener is ever refused as FULL while the live count is far
+    below max_connections, the statuses equal the sequential model's, and live stays exact."""
+    rng = np.random.default_rng(23)
+    r = _Run(cap_log2=10, max_conn=900)
+    model = oconn.TableModel(max_connections=900)
+    ids, owner = {}, {}
+    for b in range(14):
+        pool = helpers.flow_pool(rng, 300)
+        frames = helpers.flow_frames(rng, pool, 900, p_syn=0.9)
+        exp = model.process(_model_frames(frames, r.pf))
+        got = r.batch(frames)
+        assert not (got[:, 1] & 0xFF == pc.CT_FULL).any(), f"batch {b}: FULL with {len(model.present)} live"
+        _check(got, exp, ids, owner)
+        live = list(model.present.items())
+        slots = np.array([ids[mid] for _, (mid, _) in live], np.uint32)
+        r.ct.remove(r.torch.from_numpy(slots.view(np.int32)).to("cuda:0"))
+        model.remove([k for k, _ in live])
+        for _, (mid, _) in live:
+            owner.pop(ids.pop(mid), None)
+        assert r.ct.stats()["live"] == 0
