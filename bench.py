@@ -294,7 +294,7 @@ def pd_rate(cfg, d_slab, stride, d_dlen, n, d_ext, device, stream, steps, dl_le6
     prog = pc.Program.from_spec(PD_SPEC)
     ctx = pc.PacketContinue(prog, device)
     out = ctx.alloc_outputs(n, addr6=True, counters=False, conn=True)
-    ctx.run(d_slab, stride, d_dlen, n, out, stream=stream, ext=d_ext, dl_le64=dl_le64)
+    ctx.run(d_slab, stride, d_dlen, n, out, stream=stream, ext=d_ext, dl_le64=dl_le64)  # (cfg2: no ext)
     ct = pc.ConnTable(device, 26, 1 << 26)
     ent = ct.process(out, stream=stream)
     ct.process(out, out=ent, stream=stream)  # every opener now predates the batch
@@ -343,9 +343,10 @@ def main() -> None:
     ap.add_argument("--shard", choices=["contiguous", "rss"], default="contiguous",
                     help="N>1: contiguous blocks of the frame stream per rank, or Retina's symmetric RSS "
                          "hash (each connection on one rank; per-rank counts vary)")
-    ap.add_argument("--layout", choices=["auto", "mono", "split"], default="auto",
-                    help="slots wider than 64 B: monolithic, or split into 64-B head + 64-B ext slabs "
-                         "(auto = split; include/retina_pc.h)")
+    ap.add_argument("--layout", choices=["auto", "mono", "split", "compact"], default="auto",
+                    help="slots wider than 64 B: monolithic, split into 64-B head + 64-B ext slabs, or "
+                         "split with ext rows only for the frames that need them (auto = split; "
+                         "include/retina_pc.h)")
     args = ap.parse_args()
 
     import torch
@@ -383,9 +384,14 @@ def main() -> None:
     n = len(dlen)  # this rank's frames
     alg_bytes = synth.alg_read_bytes(slab, dlen, stride)
     split = stride > 64 and args.layout != "mono"
-    d_ext = None
+    compact = split and args.layout == "compact"
+    d_ext = d_chunk = None
     if split:
-        head, ext = pc.split_slab(slab, stride)
+        if compact:
+            head, ext, chunk = pc.split_slab(slab, stride, dlen, compact=True)
+            d_chunk = torch.from_numpy(chunk.view(np.int32)).to(dev)
+        else:
+            head, ext = pc.split_slab(slab, stride)
         d_slab = torch.from_numpy(head).to(dev)
         d_ext = torch.from_numpy(ext).to(dev)
         run_stride = 64
@@ -404,7 +410,7 @@ def main() -> None:
     stream = torch.cuda.current_stream(dev)
 
     for _ in range(args.warmup):
-        ctx.run(d_slab, run_stride, d_dlen, n, out, stream=stream, ext=d_ext, dl_le64=dl_le64)
+        ctx.run(d_slab, run_stride, d_dlen, n, out, stream=stream, ext=d_ext, dl_le64=dl_le64, ext_chunk=d_chunk)
     torch.cuda.synchronize(dev)
     if distributed:
         dist.barrier()
@@ -414,7 +420,7 @@ def main() -> None:
     t0 = time.perf_counter()
     ev0.record(stream)
     for _ in range(args.steps):
-        ctx.run(d_slab, run_stride, d_dlen, n, out, stream=stream, ext=d_ext, dl_le64=dl_le64)
+        ctx.run(d_slab, run_stride, d_dlen, n, out, stream=stream, ext=d_ext, dl_le64=dl_le64, ext_chunk=d_chunk)
     ev1.record(stream)
     torch.cuda.synchronize(dev)
     if distributed:
@@ -429,12 +435,12 @@ def main() -> None:
     if not args.no_conn and world == 1:
         cout = ctx.alloc_outputs(n, addr6=True, counters=False, conn=True)
         for _ in range(3):
-            ctx.run(d_slab, run_stride, d_dlen, n, cout, stream=stream, ext=d_ext, dl_le64=dl_le64)
+            ctx.run(d_slab, run_stride, d_dlen, n, cout, stream=stream, ext=d_ext, dl_le64=dl_le64, ext_chunk=d_chunk)
         c0 = torch.cuda.Event(enable_timing=True)
         c1 = torch.cuda.Event(enable_timing=True)
         c0.record(stream)
         for _ in range(args.steps):
-            ctx.run(d_slab, run_stride, d_dlen, n, cout, stream=stream, ext=d_ext, dl_le64=dl_le64)
+            ctx.run(d_slab, run_stride, d_dlen, n, cout, stream=stream, ext=d_ext, dl_le64=dl_le64, ext_chunk=d_chunk)
         c1.record(stream)
         torch.cuda.synchronize(dev)
         cms = c0.elapsed_time(c1) / args.steps
@@ -474,7 +480,7 @@ def main() -> None:
 
     # correctness totals of the last step (outside the timed region)
     cnt_out = ctx.alloc_outputs(n, addr6=True, counters=True)
-    ctx.run(d_slab, run_stride, d_dlen, n, cnt_out, stream=stream, ext=d_ext)
+    ctx.run(d_slab, run_stride, d_dlen, n, cnt_out, stream=stream, ext=d_ext, ext_chunk=d_chunk)
     torch.cuda.synchronize(dev)
     verified = verify_sample(cfg, slab, dlen, stride, cnt_out, sh.start if args.shard == "contiguous" else 0)
     counters = torch.cat([cnt_out.counters.view(torch.int32)[:3].to(torch.int64),
@@ -508,7 +514,8 @@ def main() -> None:
             "dtype": "u8",
             "data": "synthetic (seeded splitmix64 frames, retina_amd/synth.py)",
             "config": {"workload": f"{cfg}: {desc}", "frames_per_gpu": n, "stride": stride,
-                       "layout": "split (64-B head + 64-B ext slabs)" if split else f"{run_stride}-B slots",
+                       "layout": ("compact split (64-B head slab + ext rows where needed)" if compact else
+                                  "split (64-B head + 64-B ext slabs)") if split else f"{run_stride}-B slots",
                        "subscriptions": prog.info["n_subscriptions"], "tree_size": prog.info["tree_size"],
                        "parallelism": f"shard{world}",
                        "shard": {"mode": args.shard if world > 1 else "none", "frames_total": total_frames,

@@ -96,11 +96,13 @@ typedef struct rtn_conn {
 #define RTN_MAX_FRAMES (1u << 31)
 
 /* rtn_batch_t.flags */
-#define RTN_BATCH_DL_LE64 1u /* the caller asserts data_len[i] <= 64 for every frame (see below)  */
+#define RTN_BATCH_DL_LE64 1u   /* the caller asserts data_len[i] <= 64 for every frame (see below) */
+#define RTN_BATCH_EXT_COMPACT 2u /* split layout with ext rows only for the frames that need them  */
 
 /* Status bits (counters[3], rtn_pc_take_status): frames whose results are not the reference's. */
 #define RTN_STATUS_HDR_PAST_SLOT 1u /* 64-B slots, no ext: an IP frame's headers run past byte 64 */
 #define RTN_STATUS_DL_PAST_SLOT 2u  /* RTN_BATCH_DL_LE64 asserted, but a frame has data_len > 64  */
+#define RTN_STATUS_EXT_ROWS 4u      /* RTN_BATCH_EXT_COMPACT: a needed ext row is past ext_rows     */
 
 /* A batch of frames laid out for coalesced HBM reads, in one of two layouts:
  *  - monolithic (ext == NULL): slot i (stride bytes, a multiple of 64) holds the first
@@ -124,8 +126,27 @@ typedef struct rtn_batch {
   uint32_t core_id;         /* the calling lcore (passed to CoreId callbacks by the host) */
   const uint8_t* ext;       /* split layout: bytes [64, 128) of each frame, 64-byte slots */
   uint32_t flags;           /* RTN_BATCH_*                                                */
-  uint32_t reserved;        /* 0                                                          */
+  uint32_t ext_rows;        /* RTN_BATCH_EXT_COMPACT: rows in ext                         */
+  const uint32_t* ext_chunk; /* RTN_BATCH_EXT_COMPACT: [ceil(n/512)] row of the first frame of
+                                each 512-frame chunk that needs one (an exclusive prefix sum) */
 } rtn_batch_t;
+
+/* The compact split layout (RTN_BATCH_EXT_COMPACT): ext holds bytes [64, 128) only of the frames
+ * for which rtn_ext_needed() holds, one 64-byte row each, in frame order; the kernel finds frame
+ * i's row as ext_chunk[i / RTN_CHUNK_FRAMES] + (number of such frames of the chunk before i).
+ * A 128-byte HBM line then carries two needed rows instead of a needed and an unneeded one.
+ * The rule is the kernel's own (the frame's headers may pass byte 64 and the frame is longer):
+ * `head` is the frame's first 64 bytes (the head slot). A row past ext_rows is not read
+ * (RTN_STATUS_EXT_ROWS). */
+static inline int rtn_ext_needed(const uint8_t* head, uint16_t data_len) {
+  const unsigned et = ((unsigned)head[12] << 8) | head[13];
+  const int q = et == 0x8100u;
+  const unsigned inner = q ? (((unsigned)head[16] << 8) | head[17]) : et;
+  const unsigned ihl4 = (unsigned)(head[q ? 18 : 14] & 0xFu) << 2;
+  const unsigned l4 = (q ? 18u : 14u) + (inner == 0x86DDu ? 40u : ihl4);
+  const int ip = inner == 0x0800u || inner == 0x86DDu;
+  return ip && data_len > 64u && l4 + 20u > 64u;
+}
 
 /* Records are ranked per chunk of RTN_CHUNK_FRAMES frames, in frame order: the k-th forwarded
  * frame of chunk c = i / RTN_CHUNK_FRAMES (k = popcount of fwd_bitmap over the chunk's frames

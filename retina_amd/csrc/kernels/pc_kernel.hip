@@ -61,7 +61,8 @@ struct rtn_args {
   rtn_u64 stride;
   const unsigned short* dlen;
   rtn_u32 n;
-  rtn_u32 flags;              // bit0: addr6, bit1: counters, bit2: conn, bit3: caller asserts data_len <= 64
+  rtn_u32 flags;              // bit0: addr6, bit1: counters, bit2: conn, bit3: caller asserts data_len <= 64,
+                              // bit4: compact ext rows (RTN_BATCH_EXT_COMPACT)
   rtn_u64* pc_bm;             // [ceil(n/64)]  PacketContinue bit
   rtn_u64* fwd_bm;            // [ceil(n/64)]  PacketContinue && L4Context::new Ok
   rtn_l4rec* recs;            // [ceil(n/512)*512], dense per chunk
@@ -73,6 +74,9 @@ struct rtn_args {
   const unsigned char* ext;   // split layout: bytes 64..127 of each frame (64-byte slots), or null
   rtn_u64* conn;              // optional [ceil(n/512)*512] rtn_conn_t, indexed like recs (flags bit2)
   rtn_u64* conn_dlv;          // [ceil(n/512)*512][RTN_CONN_WORDS] first-packet statement masks
+  const rtn_u32* ext_chunk;   // flags bit4 (compact ext): row of each chunk's first needing frame
+  rtn_u32 ext_rows;           // ... and the rows ext holds
+  rtn_u32 pad;
 };
 
 struct rtn_view {
@@ -322,6 +326,7 @@ struct rtn_chunk {
   rtn_u32 nrec, nflushed;   // records produced / already stored in this chunk
   rtn_u32 ndlv;             // delivery records produced in this chunk
   rtn_u32 nv6, nv6flushed;  // IPv6 address records (addr6) produced / stored in this chunk
+  rtn_u32 next;             // compact ext: needing frames of this chunk so far
   rtn_u64 my_pc, my_fwd, my_dlv;  // lane k holds group k's bitmap words until the chunk ends
 };
 
@@ -580,7 +585,7 @@ __device__ __forceinline__ void rtn_run(const rtn_args& a) {
   for (rtn_u32 c = wave_g; c < nchunks; c += nwaves) {
     const rtn_u32 gb = c * RTN_CHUNK_GROUPS;
     const rtn_u32 ge = gb + RTN_CHUNK_GROUPS < nw ? gb + RTN_CHUNK_GROUPS : nw;
-    rtn_chunk ch = {(rtn_u64)c * (64u * RTN_CHUNK_GROUPS), 0u, 0u, 0u, 0u, 0u, 0ull, 0ull, 0ull};
+    rtn_chunk ch = {(rtn_u64)c * (64u * RTN_CHUNK_GROUPS), 0u, 0u, 0u, 0u, 0u, 0u, 0ull, 0ull, 0ull};
     // 64-byte slots without ext: the next group's loads are issued before this group is parsed,
     // so one group of loads is always in flight per wave (cfg2 -2.2 %, in-process A/B; with the
     // split layout's dependent ext loads it measured 5 % slower on cfg4 and is not used there)
@@ -612,10 +617,22 @@ __device__ __forceinline__ void rtn_run(const rtn_args& a) {
         for (int j = 0; j < 16; ++j) w[j] = lo[j];
 #pragma unroll
         for (int j = 16; j < 32; ++j) w[j] = 0u;
-        if (rtn_need_hi(lo, dl)) {
+        const bool need = rtn_need_hi(lo, dl);
+        // compact ext (rtn_ext_needed in retina_pc.h): the row is the chunk's first row plus the
+        // number of needing frames of the chunk before this one
+        rtn_u64 row = (rtn_u64)g * 64u + lane;
+        bool load = need;
+        if (MODE == RTN_SPLIT && (a.flags & 16u)) {
+          const rtn_u64 nm = __ballot(need);
+          row = (rtn_u64)a.ext_chunk[c] + ch.next + (rtn_u32)__popcll(nm & lane_lt);
+          ch.next += (rtn_u32)__popcll(nm);
+          load = need && row < a.ext_rows;
+          if (need && !load) acc.status |= 4u;  // RTN_STATUS_EXT_ROWS
+        }
+        if (load) {
           // bytes 64..127: the ext slot (split layout) or the slot's second half (monolithic)
           const rtn_v4u* hi = MODE == RTN_SPLIT
-                                  ? reinterpret_cast<const rtn_v4u*>(a.ext + (rtn_u64)(g * 64u + lane) * 64u)
+                                  ? reinterpret_cast<const rtn_v4u*>(a.ext + row * 64u)
                                   : reinterpret_cast<const rtn_v4u*>(a.slab + (rtn_u64)(g * 64u + lane) * a.stride) + 4;
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
@@ -640,7 +657,8 @@ __device__ __forceinline__ void rtn_run(const rtn_args& a) {
     }
   }
   // one set of atomics per wave: status bits always (RTN_STATUS_*), totals when requested
-  const rtn_u32 st = (__ballot((acc.status & 1u) != 0u) ? 1u : 0u) | (__ballot((acc.status & 2u) != 0u) ? 2u : 0u);
+  const rtn_u32 st = (__ballot((acc.status & 1u) != 0u) ? 1u : 0u) | (__ballot((acc.status & 2u) != 0u) ? 2u : 0u) |
+                     (__ballot((acc.status & 4u) != 0u) ? 4u : 0u);
   if (lane == 0u && st) atomicOr(&a.counters[3], st);
   if (!(a.flags & 2u)) return;
   rtn_u64 bytes = acc.bytes, ignored = acc.ignored, tcpb = acc.tcpb, udpb = acc.udpb;

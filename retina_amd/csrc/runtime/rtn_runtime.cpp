@@ -215,6 +215,9 @@ struct KArgs {
   const unsigned char* ext;
   rtn_conn_t* conn;
   uint64_t* conn_dlv;
+  const uint32_t* ext_chunk;
+  uint32_t ext_rows;
+  uint32_t pad;
 };
 
 // Groups per wave of a kernel (RTN_PD_GPW / RTN_CT_GPW): the default, unless an RTN_KERNEL_DEFINES
@@ -492,7 +495,9 @@ int32_t rtn_pc_set_grid(rtn_pc_t* pc, uint32_t blocks) {
 int32_t rtn_pc_run(rtn_pc_t* pc, const rtn_batch_t* in, rtn_pc_out_t* out, void* stream) {
   if (!pc || !in || !out) return fail(RTN_EINVAL, "null argument");
   if (in->n > RTN_MAX_FRAMES) return fail(RTN_EINVAL, "batch larger than RTN_MAX_FRAMES");
-  if (in->flags & ~RTN_BATCH_DL_LE64) return fail(RTN_EINVAL, "unknown rtn_batch_t flags");
+  if (in->flags & ~(RTN_BATCH_DL_LE64 | RTN_BATCH_EXT_COMPACT)) return fail(RTN_EINVAL, "unknown rtn_batch_t flags");
+  if ((in->flags & RTN_BATCH_EXT_COMPACT) && (!in->ext || !in->ext_chunk))
+    return fail(RTN_EINVAL, "RTN_BATCH_EXT_COMPACT needs ext and ext_chunk");
   if (in->n == 0) return RTN_OK;
   if (!in->slab || !in->data_len) return fail(RTN_EINVAL, "batch slab/data_len missing");
   if (in->stride < 64 || in->stride % 64 != 0) return fail(RTN_EINVAL, "stride must be a positive multiple of 64");
@@ -525,7 +530,10 @@ int32_t rtn_pc_run(rtn_pc_t* pc, const rtn_batch_t* in, rtn_pc_out_t* out, void*
   a.dlen = in->data_len;
   a.n = in->n;
   a.flags = (out->addr6 ? 1u : 0u) | (out->counters ? 2u : 0u) | (out->conn ? 4u : 0u) |
-            ((in->flags & RTN_BATCH_DL_LE64) ? 8u : 0u);
+            ((in->flags & RTN_BATCH_DL_LE64) ? 8u : 0u) | ((in->flags & RTN_BATCH_EXT_COMPACT) ? 16u : 0u);
+  a.ext_chunk = in->ext_chunk;
+  a.ext_rows = in->ext_rows;
+  a.pad = 0u;
   a.pc_bm = out->pc_bitmap;
   a.fwd_bm = out->fwd_bitmap;
   a.recs = out->l4;

@@ -31,10 +31,12 @@ class FilterError(RetinaError):
 class _Batch(C.Structure):
     _fields_ = [("slab", C.c_void_p), ("stride", C.c_uint64), ("data_len", C.c_void_p),
                 ("n", C.c_uint32), ("core_id", C.c_uint32), ("ext", C.c_void_p), ("flags", C.c_uint32),
-                ("reserved", C.c_uint32)]
+                ("ext_rows", C.c_uint32), ("ext_chunk", C.c_void_p)]
 
 
 BATCH_DL_LE64 = 1          # RTN_BATCH_DL_LE64
+BATCH_EXT_COMPACT = 2      # RTN_BATCH_EXT_COMPACT
+STATUS_EXT_ROWS = 4        # RTN_STATUS_EXT_ROWS
 STATUS_HDR_PAST_SLOT = 1   # RTN_STATUS_HDR_PAST_SLOT
 STATUS_DL_PAST_SLOT = 2    # RTN_STATUS_DL_PAST_SLOT
 COUNTERS_BYTES = 64        # RTN_COUNTERS_BYTES
@@ -438,19 +440,24 @@ class PacketContinue:
         )
 
     def run(self, slab, stride: int, data_len, n: int | None = None, out: PCOutputs | None = None,
-            stream=None, core_id: int = 0, ext=None, dl_le64: bool = False) -> PCOutputs:
+            stream=None, core_id: int = 0, ext=None, dl_le64: bool = False, ext_chunk=None) -> PCOutputs:
         """One rtn_pc_run. `ext` (device uint8, 64 B per frame) selects the split layout: `slab`
         then holds bytes [0, 64) of every frame (stride 64) and `ext` bytes [64, 128).
         dl_le64 asserts that every data_len is <= 64 (RTN_BATCH_DL_LE64), which 64-byte slots
-        without ext need unless `out` has counters (include/retina_pc.h)."""
+        without ext need unless `out` has counters (include/retina_pc.h). `ext_chunk` (device
+        uint32, one per 512-frame chunk) selects the compact split layout: `ext` then holds rows
+        only for the frames rtn_ext_needed() names (split_slab(..., compact=True))."""
         import torch
 
         if n is None:
             n = int(data_len.numel())
         if out is None or out.n < n:
             out = self.alloc_outputs(n)
+        flags = (BATCH_DL_LE64 if dl_le64 else 0) | (BATCH_EXT_COMPACT if ext_chunk is not None else 0)
+        rows = int(ext.numel()) // 64 if ext is not None else 0
         b = _Batch(slab.data_ptr(), stride, data_len.data_ptr(), n, core_id,
-                   ext.data_ptr() if ext is not None else None, BATCH_DL_LE64 if dl_le64 else 0, 0)
+                   ext.data_ptr() if ext is not None else None, flags, rows,
+                   ext_chunk.data_ptr() if ext_chunk is not None else None)
         o = _out_struct(out)
         s = stream if stream is not None else torch.cuda.current_stream(self.device)
         _check(lib().rtn_pc_run(self._h, C.byref(b), C.byref(o), C.c_void_p(s.cuda_stream)))
@@ -606,10 +613,34 @@ def decode_ct(entries, pc_out: PCOutputs) -> np.ndarray:
     return e[_fwd_index(fwd_bm, pc_out.n)]
 
 
-def split_slab(slab: np.ndarray, stride: int) -> tuple[np.ndarray, np.ndarray]:
-    """Monolithic slots of `stride` >= 128 -> the split layout (64-B head slots, 64-B ext slots)."""
+def ext_needed(head: np.ndarray, dlen: np.ndarray) -> np.ndarray:
+    """rtn_ext_needed (include/retina_pc.h) for every frame: head = [n, >= 64] first bytes."""
+    h = head.astype(np.int64)
+    et = (h[:, 12] << 8) | h[:, 13]
+    q = et == 0x8100
+    inner = np.where(q, (h[:, 16] << 8) | h[:, 17], et)
+    ihl4 = (np.where(q, h[:, 18], h[:, 14]) & 0xF) << 2
+    l4 = np.where(q, 18, 14) + np.where(inner == 0x86DD, 40, ihl4)
+    ip = (inner == 0x0800) | (inner == 0x86DD)
+    return ip & (dlen.astype(np.int64) > 64) & (l4 + 20 > 64)
+
+
+def split_slab(slab: np.ndarray, stride: int, dlen: np.ndarray | None = None, compact: bool = False):
+    """Monolithic slots of `stride` >= 128 -> the split layout (64-B head slots, 64-B ext slots):
+    (head, ext). compact=True (needs dlen) keeps ext rows only for the frames that need them
+    (RTN_BATCH_EXT_COMPACT) and returns (head, ext, ext_chunk)."""
     b = slab.reshape(-1, stride)
-    return np.ascontiguousarray(b[:, :64]).reshape(-1), np.ascontiguousarray(b[:, 64:128]).reshape(-1)
+    head = np.ascontiguousarray(b[:, :64]).reshape(-1)
+    if not compact:
+        return head, np.ascontiguousarray(b[:, 64:128]).reshape(-1)
+    need = ext_needed(b, dlen)
+    ext = np.ascontiguousarray(b[need, 64:128]).reshape(-1)
+    n = len(dlen)
+    per = np.add.reduceat(need.astype(np.int64), np.arange(0, max(n, 1), CHUNK_FRAMES)) if n else np.zeros(0, np.int64)
+    ext_chunk = np.concatenate([[0], np.cumsum(per)[:-1]]).astype(np.uint32)
+    if ext.size == 0:
+        ext = np.zeros(64, np.uint8)  # (a valid pointer; no row is read)
+    return head, ext, ext_chunk
 
 
 def pack_frames(frames, stride: int = 128) -> tuple[np.ndarray, np.ndarray]:

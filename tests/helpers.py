@@ -42,7 +42,8 @@ def oracle_run(spec: str, slab: np.ndarray, stride: int, dlen: np.ndarray) -> di
 def gpu_run(spec: str, slab: np.ndarray, stride: int, dlen: np.ndarray, device: int = 0, split: bool = False,
             conn: bool = False) -> dict:
     """Run the product on the GPU. split=True hands the frames over in the split layout
-    (64-B head slots + 64-B ext slots, include/retina_pc.h) instead of `stride`-byte slots;
+    (64-B head slots + 64-B ext slots, include/retina_pc.h) instead of `stride`-byte slots,
+    split="compact" in the compact split layout (ext rows only where rtn_ext_needed);
     conn=True also computes the connection stage (rtn_conn_t per forwarded frame)."""
     import torch
 
@@ -52,14 +53,18 @@ def gpu_run(spec: str, slab: np.ndarray, stride: int, dlen: np.ndarray, device: 
     ctx = pc.PacketContinue(prog, device)
     dev = torch.device("cuda", device)
     n = len(dlen)
-    ext_t = None
-    if split:
+    ext_t = chunk_t = None
+    if split == "compact":
+        head, ext, chunk = pc.split_slab(np.ascontiguousarray(slab, np.uint8), stride, np.asarray(dlen), compact=True)
+        slab, stride = head, 64
+        ext_t, chunk_t = torch.from_numpy(ext).to(dev), torch.from_numpy(chunk.view(np.int32)).to(dev)
+    elif split:
         head, ext = pc.split_slab(np.ascontiguousarray(slab, np.uint8), stride)
         slab, stride = head, 64
         ext_t = torch.from_numpy(ext).to(dev)
     slab_t = torch.from_numpy(np.ascontiguousarray(slab, np.uint8)).to(dev)
     dl_t = torch.from_numpy(np.ascontiguousarray(dlen, np.uint16).view(np.int16)).to(dev)
-    out = ctx.run(slab_t, stride, dl_t, n, out=ctx.alloc_outputs(max(n, 1), conn=conn), ext=ext_t)
+    out = ctx.run(slab_t, stride, dl_t, n, out=ctx.alloc_outputs(max(n, 1), conn=conn), ext=ext_t, ext_chunk=chunk_t)
     torch.cuda.synchronize()
     d = out.decode()
     cnt = out.counters_host()

@@ -20,6 +20,8 @@ def declared_functions() -> list[str]:
     for h in HEADERS:
         text = re.sub(r"/\*.*?\*/", "", h.read_text(), flags=re.S)
         names |= set(re.findall(r"\b(rtn_[a-z0-9_]+)\s*\(", text))
+        # header-only helpers (static inline) are not library symbols
+        names -= set(re.findall(r"static inline [\w\s\*]+?\b(rtn_[a-z0-9_]+)\s*\(", text))
     return sorted(names)
 
 
@@ -193,3 +195,42 @@ def test_integration_extern_fns_exist():
     hdrs = "".join(h.read_text() for h in HEADERS)
     missing = [f for f in declared if not re.search(r"\b" + f + r"\s*\(", hdrs)]
     assert declared and not missing, missing
+
+
+def test_ext_needed_rule_matches_header(tmp_path):
+    """The compact split layout depends on the caller and the kernel agreeing on which frames
+    have an ext row: rtn_ext_needed (retina_pc.h, C) and pc.ext_needed (numpy, the packer the
+    tests and the bench use) agree on every frame of the traces, adversarial and synthetic
+    corpora, and the kernel's own rule is the same expression (GPU tests: compact layout)."""
+    import subprocess
+
+    import numpy as np
+
+    from retina_amd import synth
+
+    t = np.load(Path(__file__).resolve().parent / "golden" / "traces.npz")
+    a = np.load(Path(__file__).resolve().parent / "golden" / "corpus_adversarial.npz")
+    s3, d3 = synth.cfg3(4096, start=3)
+    s4, d4 = synth.cfg4(4096, start=4)
+    slab = np.concatenate([t["slab"], a["slab"], s3, s4]).reshape(-1, 128)
+    dlen = np.concatenate([t["dlen"], a["dlen"], d3, d4])
+    (tmp_path / "in.bin").write_bytes(np.ascontiguousarray(slab[:, :64]).tobytes())
+    (tmp_path / "dl.bin").write_bytes(dlen.astype(np.uint16).tobytes())
+    src = ('#include "retina_pc.h"\n#include <stdio.h>\nint main(int c, char** v) {\n'
+           '  FILE* f = fopen(v[1], "rb"); FILE* g = fopen(v[2], "rb"); unsigned char h[64]; uint16_t d;\n'
+           '  while (fread(h, 1, 64, f) == 64 && fread(&d, 2, 1, g) == 1) putchar(rtn_ext_needed(h, d) ? 49 : 48);\n'
+           '  return 0;\n}\n')
+    (tmp_path / "en.c").write_text(src)
+    inc = Path(__file__).resolve().parent.parent / "include"
+    r = subprocess.run(["gcc", "-std=c11", "-Wall", "-Werror", f"-I{inc}", str(tmp_path / "en.c"), "-o",
+                        str(tmp_path / "en")], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    out = subprocess.run([str(tmp_path / "en"), str(tmp_path / "in.bin"), str(tmp_path / "dl.bin")],
+                         capture_output=True, text=True, check=True).stdout
+    c_rule = np.frombuffer(out.encode(), np.uint8) == ord("1")
+    assert len(c_rule) == len(dlen)
+    py_rule = pc.ext_needed(slab, dlen)
+    assert np.array_equal(c_rule, py_rule) and 0 < py_rule.sum() < len(dlen)
+    head, ext, chunk = pc.split_slab(slab.reshape(-1), 128, dlen, compact=True)
+    assert ext.size == 64 * int(py_rule.sum()) and chunk[0] == 0 and len(chunk) == (len(dlen) + 511) // 512
+    assert np.array_equal(ext.reshape(-1, 64), slab[py_rule, 64:128])

@@ -29,7 +29,7 @@ def _corpus(name: str):
     return np.concatenate([s2, s3, s4]), np.concatenate([d2, d3, d4])
 
 
-@pytest.mark.parametrize("layout", ["mono", "split"])
+@pytest.mark.parametrize("layout", ["mono", "split", "compact"])
 @pytest.mark.parametrize("corpus", ["traces", "adversarial", "synth"])
 @pytest.mark.parametrize("fset", list(SETS))
 def test_golden_fixture(fset, corpus, layout, gpu):
@@ -39,12 +39,13 @@ def test_golden_fixture(fset, corpus, layout, gpu):
     exp = {"pc": np.unpackbits(g[f"{corpus}_pc"])[:n].astype(bool),
            "fwd": np.unpackbits(g[f"{corpus}_fwd"])[:n].astype(bool),
            "rec": g[f"{corpus}_rec"], "dm": g[f"{corpus}_dm"]}
-    got = helpers.gpu_run(SETS[fset], slab, 128, dlen, split=layout == "split")
+    got = helpers.gpu_run(SETS[fset], slab, 128, dlen, split={"mono": False, "split": True, "compact": "compact"}[layout])
     helpers.assert_same(got, exp, f"{fset}/{corpus}/{layout}")
 
 
 @pytest.mark.parametrize("cfg,stride,split", [("cfg2", 64, False), ("cfg3", 128, False), ("cfg4", 128, False),
-                                              ("cfg3", 128, True), ("cfg4", 128, True)])
+                                              ("cfg3", 128, True), ("cfg4", 128, True),
+                                              ("cfg3", 128, "compact"), ("cfg4", 128, "compact")])
 def test_synthetic_vs_oracle(cfg, stride, split, gpu):
     n = (1 << 18) + 37  # ragged tail: not a multiple of 64
     gen = {"cfg2": synth.cfg2, "cfg3": synth.cfg3, "cfg4": synth.cfg4}[cfg]

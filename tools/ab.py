@@ -28,6 +28,7 @@ def main() -> None:
     ap.add_argument("--reps", type=int, default=7)
     ap.add_argument("--frames", type=int, default=0)
     ap.add_argument("--mono", action="store_true")
+    ap.add_argument("--compact", action="store_true", help="compact split layout (RTN_BATCH_EXT_COMPACT)")
     args = ap.parse_args()
     import torch
 
@@ -41,8 +42,13 @@ def main() -> None:
     slab, dlen = bench.gen_frames(args.cfg, n, 0)
     alg = synth.alg_read_bytes(slab, dlen, stride)
     dev = torch.device("cuda", 0)
-    d_ext = None
-    if stride > 64 and not args.mono:
+    d_ext = d_chunk = None
+    if stride > 64 and args.compact:
+        head, ext, chunk = pc.split_slab(slab, stride, dlen, compact=True)
+        d_slab, d_ext = torch.from_numpy(head).to(dev), torch.from_numpy(ext).to(dev)
+        d_chunk = torch.from_numpy(chunk.view(np.int32)).to(dev)
+        stride = 64
+    elif stride > 64 and not args.mono:
         head, ext = pc.split_slab(slab, stride)
         d_slab, d_ext = torch.from_numpy(head).to(dev), torch.from_numpy(ext).to(dev)
         stride = 64
@@ -68,11 +74,11 @@ def main() -> None:
     for _ in range(args.reps):
         for e, ctx in ctxs:
             for _ in range(2):
-                ctx.run(d_slab, stride, d_dlen, n, out, ext=d_ext, dl_le64=le64)
+                ctx.run(d_slab, stride, d_dlen, n, out, ext=d_ext, dl_le64=le64, ext_chunk=d_chunk)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(10):
-                ctx.run(d_slab, stride, d_dlen, n, out, ext=d_ext, dl_le64=le64)
+                ctx.run(d_slab, stride, d_dlen, n, out, ext=d_ext, dl_le64=le64, ext_chunk=d_chunk)
             e1.record()
             torch.cuda.synchronize()
             times[e].append(e0.elapsed_time(e1) / 10)
