@@ -1,6 +1,7 @@
 """In-process A/B timing of kernel variants on one GPU (tools/README.md).
 
-    python tools/ab.py cfg2|cfg3|cfg4 VARIANT[:DEFINES][@GRID] ... [--reps R] [--frames N] [--mono]
+    python tools/ab.py cfg2|cfg3|cfg4 VARIANT[:DEFINES][@GRID][#split|#compact|#mono] ... [--reps R]
+        [--frames N] [--mono] [--compact]
 
 VARIANT names a tools/variants.py function (or several joined with '+'). Prints, per entry, the
 median kernel time over R interleaved rounds of 10 launches, Mpkt/s and the HBM-read roofline
@@ -42,25 +43,27 @@ def main() -> None:
     slab, dlen = bench.gen_frames(args.cfg, n, 0)
     alg = synth.alg_read_bytes(slab, dlen, stride)
     dev = torch.device("cuda", 0)
-    d_ext = d_chunk = None
-    if stride > 64 and args.compact:
-        head, ext, chunk = pc.split_slab(slab, stride, dlen, compact=True)
-        d_slab, d_ext = torch.from_numpy(head).to(dev), torch.from_numpy(ext).to(dev)
-        d_chunk = torch.from_numpy(chunk.view(np.int32)).to(dev)
-        stride = 64
-    elif stride > 64 and not args.mono:
+    # the layouts an entry may ask for ("VARIANT#compact"): split (default for wide slots),
+    # compact split, or the monolithic slots with --mono
+    lay = {}
+    if stride > 64:
         head, ext = pc.split_slab(slab, stride)
-        d_slab, d_ext = torch.from_numpy(head).to(dev), torch.from_numpy(ext).to(dev)
-        stride = 64
-    else:
-        d_slab = torch.from_numpy(slab).to(dev)
+        lay["split"] = (torch.from_numpy(head).to(dev), 64, torch.from_numpy(ext).to(dev), None)
+        if args.compact or any(e.endswith("#compact") for e in args.entries):
+            h2, ext2, chunk = pc.split_slab(slab, stride, dlen, compact=True)
+            lay["compact"] = (lay["split"][0], 64, torch.from_numpy(ext2).to(dev),
+                              torch.from_numpy(chunk.view(np.int32)).to(dev))
+    if stride == 64 or args.mono or any(e.endswith("#mono") for e in args.entries):
+        lay["mono"] = (torch.from_numpy(slab).to(dev), stride, None, None)
+    default = "mono" if (stride == 64 or args.mono) else ("compact" if args.compact else "split")
     d_dlen = torch.from_numpy(dlen.view(np.int16)).to(dev)
-    le64 = stride == 64 and d_ext is None and int(dlen.max()) <= 64
+    le64 = stride == 64 and int(dlen.max()) <= 64
     spec = bench.spec_for(args.cfg)
     tmp = ROOT / "gpurun_out" / "variants"
     ctxs, out = [], None
     for e in args.entries:
-        name, _, grid = e.partition("@")
+        name, _, layout = e.partition("#")
+        name, _, grid = name.partition("@")
         name, _, defs = name.partition(":")
         os.environ["RTN_KERNEL_TEMPLATE"] = str(variants.write(name, tmp))
         os.environ["RTN_KERNEL_DEFINES"] = defs
@@ -68,17 +71,17 @@ def main() -> None:
         if grid:
             ctx.set_grid(int(grid))
         out = out or ctx.alloc_outputs(n, addr6=True, counters=False)
-        ctxs.append((e, ctx))
+        ctxs.append((e, ctx, lay[layout or default]))
         print("compiled", e, flush=True)
-    times = {e: [] for e, _ in ctxs}
+    times = {e: [] for e, _, _ in ctxs}
     for _ in range(args.reps):
-        for e, ctx in ctxs:
+        for e, ctx, (d_slab, st, d_ext, d_chunk) in ctxs:
             for _ in range(2):
-                ctx.run(d_slab, stride, d_dlen, n, out, ext=d_ext, dl_le64=le64, ext_chunk=d_chunk)
+                ctx.run(d_slab, st, d_dlen, n, out, ext=d_ext, dl_le64=le64 and d_ext is None, ext_chunk=d_chunk)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(10):
-                ctx.run(d_slab, stride, d_dlen, n, out, ext=d_ext, dl_le64=le64, ext_chunk=d_chunk)
+                ctx.run(d_slab, st, d_dlen, n, out, ext=d_ext, dl_le64=le64 and d_ext is None, ext_chunk=d_chunk)
             e1.record()
             torch.cuda.synchronize()
             times[e].append(e0.elapsed_time(e1) / 10)
