@@ -219,35 +219,70 @@ def load_traffic(cfg: str, n: int):
 
 
 def e2e_rate(ctx, slab: np.ndarray, dlen: np.ndarray, stride: int, dev, chunk: int = 1 << 21,
-             nstreams: int = 4, dl_le64: bool = False) -> dict:
-    """End-to-end rate from pinned host memory: H2D of the header slab + data_len, the kernel,
-    D2H of the bitmaps and L4Context records, pipelined over chunks on `nstreams` streams."""
+             nstreams: int = 4, dl_le64: bool = False, compact: bool = False) -> dict:
+    """End-to-end rate from pinned host memory, pipelined over chunks on `nstreams` streams: H2D
+    of the frames in the layout the kernel reads (64-B slots; or, for wider slots, the compact
+    split layout: 64-B head slots + ext rows where rtn_ext_needed + per-chunk first rows) and
+    data_len, the kernel, D2H of the bitmaps, L4Context records and (wide slots) IPv6 addresses."""
     import torch
 
+    from retina_amd import pc
+
     n = len(dlen)
-    h_slab = torch.from_numpy(slab).pin_memory()
+    wide = stride > 64
+    if wide and compact:
+        head, ext, ext_chunk = pc.split_slab(slab, stride, dlen, compact=True)
+        rows_total = int(pc.ext_needed(slab.reshape(-1, stride), dlen).sum())
+        h_slab = torch.from_numpy(head).pin_memory()
+        h_ext = torch.from_numpy(ext).pin_memory()
+        run_stride = 64
+    else:
+        h_slab = torch.from_numpy(slab).pin_memory()
+        run_stride = stride
     h_dlen = torch.from_numpy(dlen.view(np.int16)).pin_memory()
+    starts = list(range(0, n, chunk))
+    plan = []  # per chunk: (frame start, frames, ext row start, ext rows, pinned rebased ext_chunk)
+    for s in starts:
+        m = min(chunk, n - s)
+        if wide and compact:
+            c0, c1 = s // pc.CHUNK_FRAMES, (s + m + pc.CHUNK_FRAMES - 1) // pc.CHUNK_FRAMES
+            r0 = int(ext_chunk[c0])
+            r1 = int(ext_chunk[c1]) if c1 < len(ext_chunk) else rows_total
+            plan.append((s, m, r0, r1 - r0, torch.from_numpy((ext_chunk[c0:c1] - r0).astype(np.uint32).view(np.int32)).pin_memory()))
+        else:
+            plan.append((s, m, 0, 0, None))
     streams = [torch.cuda.Stream(dev) for _ in range(nstreams)]
     bufs = []
     for _ in range(nstreams):
-        bufs.append((torch.empty(chunk * stride, dtype=torch.uint8, device=dev),
-                     torch.empty(chunk, dtype=torch.int16, device=dev), ctx.alloc_outputs(chunk, addr6=False, counters=False)))
-    h_out = [torch.empty(bufs[0][2].l4.numel(), dtype=torch.uint8).pin_memory() for _ in range(nstreams)]
-    h_bm = [torch.empty(bufs[0][2].pc_bitmap.numel() * 2, dtype=torch.uint8).pin_memory() for _ in range(nstreams)]
+        bufs.append((torch.empty(chunk * run_stride, dtype=torch.uint8, device=dev),
+                     torch.empty(chunk, dtype=torch.int16, device=dev),
+                     torch.empty(chunk * 64 if wide and compact else 64, dtype=torch.uint8, device=dev),
+                     torch.empty(chunk // pc.CHUNK_FRAMES + 1, dtype=torch.int32, device=dev),
+                     ctx.alloc_outputs(chunk, addr6=wide, counters=False)))
+    h_out = [torch.empty(bufs[0][4].l4.numel(), dtype=torch.uint8).pin_memory() for _ in range(nstreams)]
+    h_bm = [torch.empty(bufs[0][4].pc_bitmap.numel() * 2, dtype=torch.uint8).pin_memory() for _ in range(nstreams)]
+    h_a6 = [torch.empty(bufs[0][4].addr6.numel(), dtype=torch.uint8).pin_memory() for _ in range(nstreams)] if wide else None
 
     def one_pass():
-        for k, s in enumerate(range(0, n, chunk)):
-            m = min(chunk, n - s)
+        for k, (s, m, r0, nr, ch) in enumerate(plan):
             st = streams[k % nstreams]
-            d_slab, d_dlen, out = bufs[k % nstreams]
+            d_slab, d_dlen, d_ext, d_chunk, out = bufs[k % nstreams]
             with torch.cuda.stream(st):
-                d_slab[:m * stride].copy_(h_slab[s * stride:(s + m) * stride], non_blocking=True)
+                d_slab[:m * run_stride].copy_(h_slab[s * run_stride:(s + m) * run_stride], non_blocking=True)
                 d_dlen[:m].copy_(h_dlen[s:s + m], non_blocking=True)
-                ctx.run(d_slab, stride, d_dlen, m, out, stream=st, dl_le64=dl_le64)
+                if ch is not None:
+                    if nr:
+                        d_ext[:nr * 64].copy_(h_ext[r0 * 64:(r0 + nr) * 64], non_blocking=True)
+                    d_chunk[:len(ch)].copy_(ch, non_blocking=True)
+                    ctx.run(d_slab, 64, d_dlen, m, out, stream=st, ext=d_ext[:max(nr, 1) * 64], ext_chunk=d_chunk)
+                else:
+                    ctx.run(d_slab, run_stride, d_dlen, m, out, stream=st, dl_le64=dl_le64)
                 h_out[k % nstreams].copy_(out.l4, non_blocking=True)
                 nb = out.pc_bitmap.numel()
                 h_bm[k % nstreams][:nb].copy_(out.pc_bitmap, non_blocking=True)
                 h_bm[k % nstreams][nb:].copy_(out.fwd_bitmap, non_blocking=True)
+                if wide:
+                    h_a6[k % nstreams].copy_(out.addr6, non_blocking=True)
 
     one_pass()
     torch.cuda.synchronize(dev)
@@ -257,10 +292,11 @@ def e2e_rate(ctx, slab: np.ndarray, dlen: np.ndarray, stride: int, dev, chunk: i
         one_pass()
     torch.cuda.synchronize(dev)
     dt = (time.perf_counter() - t0) / reps
+    layout = "compact split" if wide and compact else f"{run_stride}-B slots"
     return {"mpps": round(n / dt / 1e6, 1), "seconds_per_batch": round(dt, 4), "chunk_frames": chunk,
-            "streams": nstreams,
-            "note": "pinned host -> HBM copy of the header slab + data_len, kernel, D2H of bitmaps and L4 records; "
-                    "PCIe-bound"}
+            "streams": nstreams, "layout": layout,
+            "note": f"pinned host -> HBM copy of the frames ({layout}) + data_len, kernel, D2H of bitmaps, "
+                    "L4 records" + (" and IPv6 addresses" if wide else "") + "; PCIe-bound"}
 
 
 # Packet-level subscriptions that match at the protocol/session layer: their packets are
@@ -345,7 +381,7 @@ def main() -> None:
                          "hash (each connection on one rank; per-rank counts vary)")
     ap.add_argument("--layout", choices=["auto", "mono", "split", "compact"], default="auto",
                     help="slots wider than 64 B: monolithic, split into 64-B head + 64-B ext slabs, or "
-                         "split with ext rows only for the frames that need them (auto = split; "
+                         "split with ext rows only for the frames that need them (auto = compact; "
                          "include/retina_pc.h)")
     args = ap.parse_args()
 
@@ -384,7 +420,8 @@ def main() -> None:
     n = len(dlen)  # this rank's frames
     alg_bytes = synth.alg_read_bytes(slab, dlen, stride)
     split = stride > 64 and args.layout != "mono"
-    compact = split and args.layout == "compact"
+    # auto = the compact split layout (in-process A/B: cfg3 0.3033 -> 0.2685 ms, cfg4 0.2053 -> 0.2010)
+    compact = split and args.layout in ("compact", "auto")
     d_ext = d_chunk = None
     if split:
         if compact:
@@ -499,7 +536,7 @@ def main() -> None:
             cpu = cpu_baseline(cfg, slab, dlen, stride)
         e2e = None
         if not args.no_e2e and world == 1:
-            e2e = e2e_rate(ctx, slab, dlen, stride, dev, dl_le64=dl_le64)
+            e2e = e2e_rate(ctx, slab, dlen, stride, dev, dl_le64=dl_le64, compact=compact or stride == 64)
         line = {
             "metric": METRIC,
             "value": round(value, 1),
