@@ -1,13 +1,15 @@
 // rtn_offline: the batched offline runtime (core/src/runtime/offline.rs:39-95) on the C ABI, in C++.
 //
 //   rtn_offline <spec.toml> <capture.pcap|pcapng> [--batch N] [--mtu M] [--device D] [--no-ct]
-//               [--ct-log2 L] [--max-conn C] [--dump FILE]
+//               [--ct-log2 L] [--max-conn C] [--dump FILE] [--layout compact|mono]
 //
 // The reference's offline loop reads a capture frame by frame, skips frames longer than the
 // mtu, wraps each in an Mbuf and calls Subscription::process_packet, which runs packet_continue,
 // L4Context::new and ConnTracker::process. Here the same work runs per batch:
 //
-//   rtn_pcap_next_batch   capture -> pinned slot slab (offline.rs:64-75 rules)
+//   rtn_pcap_next_batch_split   capture -> pinned compact split layout: 64-B head slots + ext rows
+//                         only for frames whose headers may pass byte 64 (offline.rs:64-75 rules;
+//                         --layout mono: rtn_pcap_next_batch into 128-B slots)
 //   hipMemcpyAsync        slab + data_len -> HBM
 //   rtn_pc_run            packet_continue + L4Context::new + connection stage (one launch)
 //   rtn_ct_process        the ConnTracker table step (two launches; HBM-resident table)
@@ -69,7 +71,10 @@ T* host_alloc(size_t bytes) {
 constexpr uint64_t kStride = 128;  // every header the parse can reach (98 B max) fits
 
 struct HostSet {  // one batch in flight: pinned input and result buffers
-  uint8_t* slab;
+  uint8_t* slab;        // 128-B slots (mono) or 64-B head slots (compact)
+  uint8_t* ext;         // compact: ext rows
+  uint32_t* ext_chunk;  // compact: first row of each 512-frame chunk
+  uint32_t rows = 0;
   uint16_t* dlen;
   uint64_t* fwd;
   uint64_t* pcbm;
@@ -134,13 +139,14 @@ void walk(const HostSet& h, bool with_ct, Totals& t, FILE* dump) {
 int main(int argc, char** argv) {
   if (argc < 3) {
     fprintf(stderr, "usage: rtn_offline <spec.toml> <capture> [--batch N] [--mtu M] [--device D] [--no-ct] "
-                    "[--ct-log2 L] [--max-conn C] [--dump FILE]\n");
+                    "[--ct-log2 L] [--max-conn C] [--dump FILE] [--layout compact|mono]\n");
     return 2;
   }
   uint32_t batch = 1u << 20, mtu = 9702, ct_log2 = 24, max_conn = 10000000;  // configs/offline.toml
   int device = 0;
   bool with_ct = true;
   const char* dump_path = nullptr;
+  bool compact = true;
   for (int a = 3; a < argc; ++a) {
     std::string s = argv[a];
     auto next = [&]() { return a + 1 < argc ? argv[++a] : (die("missing argument value", -22), nullptr); };
@@ -151,6 +157,11 @@ int main(int argc, char** argv) {
     else if (s == "--ct-log2") ct_log2 = (uint32_t)strtoul(next(), nullptr, 10);
     else if (s == "--max-conn") max_conn = (uint32_t)strtoul(next(), nullptr, 10);
     else if (s == "--dump") dump_path = next();
+    else if (s == "--layout") {
+      const std::string l = next();
+      if (l != "compact" && l != "mono") die("--layout compact|mono", -22);
+      compact = l == "compact";
+    }
     else die(("unknown option " + s).c_str(), -22);
   }
   batch = (batch + RTN_CHUNK_FRAMES - 1) / RTN_CHUNK_FRAMES * RTN_CHUNK_FRAMES;
@@ -175,7 +186,11 @@ int main(int argc, char** argv) {
 
   // device buffers (one set: the stream orders the batches)
   const size_t bm = rtn_out_bitmap_bytes(batch), l4b = rtn_out_l4_bytes(batch), a6b = rtn_out_addr6_bytes(batch);
-  uint8_t* d_slab = dev_alloc<uint8_t>(batch * kStride);
+  const uint64_t stride = compact ? 64u : kStride;
+  const uint32_t nchunks = batch / RTN_CHUNK_FRAMES;
+  uint8_t* d_slab = dev_alloc<uint8_t>(batch * stride);
+  uint8_t* d_ext = compact ? dev_alloc<uint8_t>((size_t)batch * 64u) : nullptr;
+  uint32_t* d_chunk = compact ? dev_alloc<uint32_t>(nchunks * 4u) : nullptr;
   uint16_t* d_dlen = dev_alloc<uint16_t>(batch * 2u);
   rtn_pc_out_t out = {};
   out.pc_bitmap = dev_alloc<uint64_t>(bm);
@@ -194,7 +209,9 @@ int main(int argc, char** argv) {
   }
   HostSet hs[2];
   for (auto& h : hs) {
-    h.slab = host_alloc<uint8_t>(batch * kStride);
+    h.slab = host_alloc<uint8_t>(batch * stride);
+    h.ext = compact ? host_alloc<uint8_t>((size_t)batch * 64u) : nullptr;
+    h.ext_chunk = compact ? host_alloc<uint32_t>(nchunks * 4u) : nullptr;
     h.dlen = host_alloc<uint16_t>(batch * 2u);
     h.fwd = host_alloc<uint64_t>(bm);
     h.pcbm = host_alloc<uint64_t>(bm);
@@ -226,7 +243,10 @@ int main(int argc, char** argv) {
     }
     uint32_t n = 0;
     const auto tp = now();
-    RTN_CHECK(rtn_pcap_next_batch(cap, h.slab, kStride, h.dlen, batch, &n));
+    if (compact)
+      RTN_CHECK(rtn_pcap_next_batch_split(cap, h.slab, h.ext, batch, h.ext_chunk, h.dlen, batch, &n, &h.rows));
+    else
+      RTN_CHECK(rtn_pcap_next_batch(cap, h.slab, kStride, h.dlen, batch, &n));
     t_pack += secs_since(tp);
     if (n == 0) break;
     h.n = n;
@@ -234,9 +254,18 @@ int main(int argc, char** argv) {
     next_frame += n;
     t.frames += n;
     const size_t nbm = rtn_out_bitmap_bytes(n);
-    HIP_CHECK(hipMemcpyAsync(d_slab, h.slab, (size_t)n * kStride, hipMemcpyHostToDevice, stream));
+    HIP_CHECK(hipMemcpyAsync(d_slab, h.slab, (size_t)n * stride, hipMemcpyHostToDevice, stream));
     HIP_CHECK(hipMemcpyAsync(d_dlen, h.dlen, (size_t)n * 2u, hipMemcpyHostToDevice, stream));
-    rtn_batch_t b = {d_slab, kStride, d_dlen, n, 0u, nullptr};
+    rtn_batch_t b = {d_slab, stride, d_dlen, n, 0u, nullptr, 0u, 0u, nullptr};
+    if (compact) {
+      if (h.rows) HIP_CHECK(hipMemcpyAsync(d_ext, h.ext, (size_t)h.rows * 64u, hipMemcpyHostToDevice, stream));
+      HIP_CHECK(hipMemcpyAsync(d_chunk, h.ext_chunk, ((n + RTN_CHUNK_FRAMES - 1) / RTN_CHUNK_FRAMES) * 4u,
+                               hipMemcpyHostToDevice, stream));
+      b.ext = d_ext;
+      b.ext_rows = h.rows;
+      b.ext_chunk = d_chunk;
+      b.flags = RTN_BATCH_EXT_COMPACT;
+    }
     RTN_CHECK(rtn_pc_run(pc, &b, &out, stream));
     if (with_ct) RTN_CHECK(rtn_ct_process(ct, &out, n, d_ct, stream));
     HIP_CHECK(hipMemcpyAsync(h.fwd, out.fwd_bitmap, nbm, hipMemcpyDeviceToHost, stream));
@@ -265,13 +294,13 @@ int main(int argc, char** argv) {
   printf("{\"frames_read\": %llu, \"skipped_mtu\": %llu, \"frames\": %llu, \"bytes\": %llu, \"packet_continue\": %llu, "
          "\"forwarded\": %llu, \"tcp\": %llu, \"udp\": %llu, \"ct\": {\"hit\": %llu, \"new\": %llu, \"miss\": %llu, "
          "\"new_dropped\": %llu, \"full\": %llu, \"collision\": %llu, \"prior\": %llu, \"live\": %u}, "
-         "\"seconds\": %.6f, \"mpps\": %.2f, \"batch\": %u, "
+         "\"seconds\": %.6f, \"mpps\": %.2f, \"batch\": %u, \"layout\": \"%s\", "
          "\"host_s\": {\"pack\": %.4f, \"wait\": %.4f, \"walk\": %.4f}}\n",
          (unsigned long long)ps.frames, (unsigned long long)ps.skipped_mtu, (unsigned long long)t.frames,
          (unsigned long long)ps.bytes, (unsigned long long)t.pc, (unsigned long long)t.fwd, (unsigned long long)t.tcp,
          (unsigned long long)t.udp, (unsigned long long)t.status[1], (unsigned long long)t.status[2],
          (unsigned long long)t.status[3], (unsigned long long)t.status[4], (unsigned long long)t.status[5],
-         (unsigned long long)t.status[6], (unsigned long long)t.prior, cs.live, secs, t.frames / secs / 1e6, batch, t_pack, t_wait,
+         (unsigned long long)t.status[6], (unsigned long long)t.prior, cs.live, secs, t.frames / secs / 1e6, batch, compact ? "compact" : "mono", t_pack, t_wait,
          t_walk);
   if (dump) fclose(dump);
   rtn_pcap_close(cap);

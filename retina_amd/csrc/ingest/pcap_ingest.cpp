@@ -182,6 +182,53 @@ int32_t rtn_pcap_next_batch(rtn_pcap_t* p, uint8_t* slab, uint64_t stride, uint1
   return RTN_OK;
 }
 
+int32_t rtn_pcap_next_batch_split(rtn_pcap_t* p, uint8_t* head, uint8_t* ext, uint32_t ext_cap, uint32_t* ext_chunk,
+                                  uint16_t* data_len, uint32_t cap, uint32_t* n, uint32_t* rows) {
+  if (!p || !head || !ext || !ext_chunk || !data_len || !n || !rows) return rtn::set_error(RTN_EINVAL, "null argument");
+  prefault(p, p->off, (size_t)cap * (p->st.packed ? p->st.bytes / p->st.packed + 32u : 128u) + (1u << 20));
+  uint32_t k = 0, r = 0;
+  while (k < cap) {
+    const uint8_t* data;
+    uint32_t caplen, origlen;
+    const size_t at = p->off;
+    if (!next_frame(p, data, caplen, origlen)) break;
+    p->st.frames++;
+    if (origlen > p->mtu) {  // offline.rs:68-70
+      p->st.skipped_mtu++;
+      continue;
+    }
+    if (caplen > 0xFFFFu) {
+      p->off = at;
+      p->st.frames--;
+      *n = k;
+      *rows = r;
+      return rtn::set_error(RTN_ERANGE, "captured frame longer than 65535 bytes");
+    }
+    uint8_t* h = head + (uint64_t)k * 64u;
+    memcpy(h, data, caplen < 64u ? caplen : 64u);
+    const bool need = rtn_ext_needed(h, (uint16_t)caplen);
+    if (need && r == ext_cap) {  // no row left: end the batch before this frame
+      p->off = at;
+      p->st.frames--;
+      break;
+    }
+    if (k % RTN_CHUNK_FRAMES == 0) ext_chunk[k / RTN_CHUNK_FRAMES] = r;
+    if (need) {
+      const uint32_t m = caplen - 64u < 64u ? caplen - 64u : 64u;
+      memcpy(ext + (uint64_t)r * 64u, data + 64, m);
+      if (m < 64u) memset(ext + (uint64_t)r * 64u + m, 0, 64u - m);
+      ++r;
+    }
+    data_len[k] = (uint16_t)caplen;
+    p->st.packed++;
+    p->st.bytes += caplen;
+    ++k;
+  }
+  *n = k;
+  *rows = r;
+  return RTN_OK;
+}
+
 int32_t rtn_pcap_stats(const rtn_pcap_t* p, rtn_pcap_stats_t* st) {
   if (!p || !st) return rtn::set_error(RTN_EINVAL, "null argument");
   *st = p->st;

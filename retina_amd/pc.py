@@ -109,6 +109,8 @@ EXPORTS = {
     "rtn_pcap_open": (C.c_int32, [C.c_char_p, C.c_uint32, C.POINTER(C.c_void_p)]),
     "rtn_pcap_next_batch": (C.c_int32, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint32,
                                         C.POINTER(C.c_uint32)]),
+    "rtn_pcap_next_batch_split": (C.c_int32, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p,
+                                              C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
     "rtn_pcap_stats": (C.c_int32, [C.c_void_p, C.POINTER(_PcapStats)]),
     "rtn_pcap_rewind": (C.c_int32, [C.c_void_p]),
     "rtn_pcap_close": (None, [C.c_void_p]),
@@ -677,6 +679,18 @@ class PcapReader:
         n = C.c_uint32()
         _check(lib().rtn_pcap_next_batch(self._h, slab.ctypes.data, stride, data_len.ctypes.data, cap, C.byref(n)))
         return n.value
+
+    def next_batch_split(self, head: np.ndarray, ext: np.ndarray, ext_chunk: np.ndarray,
+                         data_len: np.ndarray) -> tuple[int, int]:
+        """The compact split layout (RTN_BATCH_EXT_COMPACT): head (uint8, cap*64), ext (uint8,
+        rows*64), ext_chunk (uint32, ceil(cap/512)), data_len (uint16[cap]) -> (frames, ext rows)."""
+        cap = len(data_len)
+        assert head.size >= cap * 64 and ext.size % 64 == 0 and ext_chunk.size >= (cap + CHUNK_FRAMES - 1) // CHUNK_FRAMES
+        n, rows = C.c_uint32(), C.c_uint32()
+        _check(lib().rtn_pcap_next_batch_split(self._h, head.ctypes.data, ext.ctypes.data, ext.size // 64,
+                                               ext_chunk.ctypes.data, data_len.ctypes.data, cap, C.byref(n),
+                                               C.byref(rows)))
+        return n.value, rows.value
 
     def rewind(self) -> None:
         _check(lib().rtn_pcap_rewind(self._h))

@@ -120,3 +120,52 @@ def test_reference_traces(reference_dir):
         if t.stat().st_size < 64:
             continue
         _check_against_oracle(t, 9702, 128)
+
+
+@pytest.mark.parametrize("ext_cap", [None, 7])
+def test_split_batches_match_the_slot_layout(tmp_path, ext_cap):
+    """rtn_pcap_next_batch_split packs the compact split layout (retina_pc.h
+    RTN_BATCH_EXT_COMPACT): the same frames as rtn_pcap_next_batch, their head slots, ext rows
+    exactly for the frames rtn_ext_needed names, in order, and per-chunk first rows; with few
+    rows (ext_cap) a batch ends early at a frame and the next one resumes there."""
+    import corpus as C
+
+    frames = [(f, len(f)) for f in C.base_frames() * 30 + C.adversarial()[:400]]
+    frames += [(f + bytes(600), len(f) + 600) for f in C.base_frames()]  # long frames: ext rows
+    p = tmp_path / "c.pcap"
+    _write_pcap(p, frames)
+    slab, dlen = pc.PcapReader(p).read_all(stride=128)
+    need = pc.ext_needed(slab.reshape(-1, 128), dlen)
+    assert need.any()
+    r = pc.PcapReader(p)
+    cap = 600
+    got_head, got_dl, got_ext, got_need = [], [], [], []
+    while True:
+        head = np.zeros(cap * 64, np.uint8)
+        ext = np.zeros((ext_cap or cap) * 64, np.uint8)
+        ch = np.zeros((cap + 511) // 512, np.uint32)
+        d = np.zeros(cap, np.uint16)
+        k, rows = r.next_batch_split(head, ext, ch, d)
+        if k == 0:
+            break
+        hb = head[:k * 64].reshape(k, 64)
+        nd = pc.ext_needed(np.pad(hb, ((0, 0), (0, 64))), d[:k])
+        assert rows == nd.sum() and (ext_cap is None or rows <= ext_cap)
+        for c in range(len(ch)):
+            if c * 512 < k:
+                assert ch[c] == nd[:c * 512].sum()
+        got_head.append(hb)
+        got_dl.append(d[:k])
+        got_ext.append(ext[:rows * 64].reshape(rows, 64))
+        got_need.append(nd)
+    assert np.array_equal(np.concatenate(got_dl), dlen)
+    assert np.array_equal(np.concatenate(got_need), need)
+    full = slab.reshape(-1, 128)
+    heads = np.concatenate(got_head)
+    for i in range(len(dlen)):
+        k = min(int(dlen[i]), 64)
+        assert heads[i, :k].tobytes() == full[i, :k].tobytes()
+    exts = np.concatenate(got_ext)
+    for j, i in enumerate(np.nonzero(need)[0]):
+        k = min(int(dlen[i]), 128) - 64
+        assert exts[j, :k].tobytes() == full[i, 64:64 + k].tobytes()

@@ -36,7 +36,8 @@ def test_offline_runtime_is_built():
 
 
 @pytest.mark.gpu
-def test_offline_runtime_vs_oracle(gpu, tmp_path):
+@pytest.mark.parametrize("layout", ["compact", "mono"])
+def test_offline_runtime_vs_oracle(gpu, tmp_path, layout):
     rng = np.random.default_rng(3)
     pool = helpers.flow_pool(rng, 700)
     frames = helpers.flow_frames(rng, pool, 9000, p_syn=0.3)
@@ -55,9 +56,10 @@ def test_offline_runtime_vs_oracle(gpu, tmp_path):
     dump = tmp_path / "dump.txt"
     batch = 2048
     r = subprocess.run([str(EXE), str(spec), str(cap), "--batch", str(batch), "--mtu", "1500", "--ct-log2", "16",
-                        "--dump", str(dump)], capture_output=True, text=True, timeout=120)
+                        "--dump", str(dump), "--layout", layout], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     summary = json.loads(r.stdout.strip().splitlines()[-1])
+    assert summary["layout"] == layout
 
     kept = [f for f, orig in caps if orig <= 1500]
     assert summary["frames"] == len(kept) and summary["skipped_mtu"] == len(caps) - len(kept)
