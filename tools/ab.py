@@ -37,7 +37,10 @@ def main() -> None:
     import variants
     from retina_amd import pc, synth
 
-    pc._LIB_PATH = pc._LIB_PATH.with_name("libretina_pc_exp.so")  # the experiments build
+    exp = pc._LIB_PATH.with_name("libretina_pc_exp.so")  # the experiments build
+    if not exp.exists() or exp.stat().st_mtime < pc._LIB_PATH.stat().st_mtime:
+        raise SystemExit("libretina_pc_exp.so is missing or older than libretina_pc.so: run tools/build_experiments.py")
+    pc._LIB_PATH = exp
     _, stride, n, _ = bench.CONFIGS[args.cfg]
     n = args.frames or n
     slab, dlen = bench.gen_frames(args.cfg, n, 0)
