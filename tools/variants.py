@@ -78,7 +78,18 @@ def noext(src: str) -> str:
     return _sub(src, "const bool need = rtn_need_hi(lo, dl);", "const bool need = rtn_need_hi(lo, dl) && a.n == 0u;")
 
 
-VARIANTS.update({"dense": dense, "nobitmaps": nobitmaps, "bm128": bm128, "noext": noext})
+def tstores(src: str) -> str:
+    """Record-block stores through the caches (plain) instead of non-temporal."""
+    return _sub(src, "#define RTN_ST(p, v) __builtin_nontemporal_store((v), (p))", "#define RTN_ST(p, v) (*(p) = (v))")
+
+
+def noconn(src: str) -> str:
+    """Timing only: the connection-stage code compiled out (register pressure without it)."""
+    return src.replace("if (a.flags & 4u) {", "if (false) {")
+
+
+VARIANTS.update({"dense": dense, "nobitmaps": nobitmaps, "bm128": bm128, "noext": noext, "tstores": tstores,
+                 "noconn": noconn})
 
 
 def write(name: str, outdir: Path) -> Path:
