@@ -244,23 +244,37 @@ def full_source(tree: PacketTree) -> tuple[str, int]:
     return src, nd
 
 
+def _host_cpu() -> str:
+    try:
+        info = Path("/proc/cpuinfo").read_text()
+        model = next((l for l in info.splitlines() if l.startswith("model name")), "")
+        flags = next((l for l in info.splitlines() if l.startswith("flags")), "")
+        return model + flags
+    except OSError:
+        return ""
+
+
 class OracleLib:
     """A generated-and-compiled oracle for one subscription set."""
 
     def __init__(self, tree: PacketTree):
         self.tree = tree
         src, self.nd = full_source(tree)
-        h = hashlib.sha1(src.encode()).hexdigest()[:16]
+        # -march=native: the build is keyed by the host CPU too, so a library built on another
+        # machine (oracle/_build/ travels with the tree) is never loaded where it may not run
+        h = hashlib.sha1((src + _host_cpu()).encode()).hexdigest()[:16]
         BUILD.mkdir(exist_ok=True)
         so = BUILD / f"pc_oracle_{h}.so"
         if not so.exists():
-            c = BUILD / f"pc_oracle_{h}.c"
+            # per-process temporaries: several ranks may build the same oracle at once
+            c = BUILD / f"pc_oracle_{h}.{os.getpid()}.c"
             c.write_text(src)
             tmp = so.with_suffix(f".{os.getpid()}.tmp")
             cc = os.environ.get("CC", "gcc")
             subprocess.run([cc, "-O3", "-march=native", "-fPIC", "-shared", "-pthread", str(c), "-o", str(tmp)],
                            check=True, capture_output=True)
             os.replace(tmp, so)
+            c.unlink(missing_ok=True)
         self.lib = C.CDLL(str(so))
         self.lib.oracle_eval.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p,
                                          C.c_void_p, C.c_void_p]
