@@ -88,8 +88,18 @@ def noconn(src: str) -> str:
     return src.replace("if (a.flags & 4u) {", "if (false) {")
 
 
+def _store_asm(mods: str):
+    def v(src: str) -> str:
+        return _sub(src, "#define RTN_ST(p, v) __builtin_nontemporal_store((v), (p))",
+                    '#define RTN_ST(p, v) asm volatile("global_store_dwordx4 %0, %1, off ' + mods +
+                    '" ::"v"(p), "v"(v) : "memory")')
+    v.__doc__ = f"Record-block stores as global_store_dwordx4 ... {mods}."
+    return v
+
+
 VARIANTS.update({"dense": dense, "nobitmaps": nobitmaps, "bm128": bm128, "noext": noext, "tstores": tstores,
-                 "noconn": noconn})
+                 "noconn": noconn, "st_sc1": _store_asm("sc1"), "st_sc0sc1": _store_asm("sc0 sc1"),
+                 "st_ntsc1": _store_asm("nt sc1"), "st_nt": _store_asm("nt")})
 
 
 def write(name: str, outdir: Path) -> Path:
