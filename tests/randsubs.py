@@ -17,7 +17,24 @@ V6 = ["2001:db8::1", "2001:db8::2", "2001:db8::/32", "::1", "fe80::/10", "::/0"]
 L7 = ["tls", "dns", "http", "quic", "ssh", "tls.sni ~ 'x'", "http.user_agent = 'curl'", "dns.query_domain ~ 'a'"]
 
 
+# every spelling grammar.pest accepts for an operator (core/src/filter/grammar.pest:57-75)
+_OPS = {"=": ["="], "!=": ["!=", "ne"], ">=": [">=", "ge"], "<=": ["<=", "le"], ">": [">", "gt"], "<": ["<", "lt"],
+        "in": ["in"]}
+
+
+def _spell(rng: random.Random, pred: str) -> str:
+    """Re-spell the operator of `proto.field OP value` with one of its grammar synonyms."""
+    parts = pred.split(" ")
+    if len(parts) >= 3 and parts[1] in _OPS:
+        parts[1] = rng.choice(_OPS[parts[1]])
+    return " ".join(parts)
+
+
 def _pred(rng: random.Random) -> str:
+    return _spell(rng, _pred0(rng))
+
+
+def _pred0(rng: random.Random) -> str:
     k = rng.randrange(14)
     p = rng.choice(PORTS)
     if k == 0:
@@ -58,9 +75,9 @@ def _filter(rng: random.Random) -> str:
         return ""
     terms = []
     for _ in range(rng.randint(1, 3)):
-        conj = " and ".join(_pred(rng) for _ in range(rng.randint(1, 3)))
+        conj = f" {rng.choice(['and', 'and', '&&', 'AND'])} ".join(_pred(rng) for _ in range(rng.randint(1, 3)))
         terms.append(f"({conj})" if rng.random() < 0.3 else conj)
-    return " or ".join(terms)
+    return f" {rng.choice(['or', 'or', '||', 'OR'])} ".join(terms)
 
 
 DTS = [["ConnRecord"], ["ZcFrame"], ["Payload"], ["ZcFrame", "FilterStr"], ["Payload", "CoreId"],
