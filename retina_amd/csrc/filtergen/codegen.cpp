@@ -329,7 +329,7 @@ struct Gen {
       if (k >= prog.delivers.size() || prog.delivers[k].sub_id != (uint32_t)dv.id)
         throw FilterError("internal: packet-continue statement order");
       std::string reach = prog.delivers[k].payload ? "(" + R + " && v.payload_ok)" : R;
-      hip += "  dm[" + std::to_string(k / 64) + "] |= " + reach + " ? (1ull << " + std::to_string(k % 64) + ") : 0ull;\n";
+      hip += "  RTN_DM_SET(dm, " + std::to_string(k / 64) + ", " + std::to_string(k % 64) + ", " + reach + ");\n";
     }
   }
   void pc_flat(const PNode& n, const std::string& R) {
@@ -377,7 +377,7 @@ struct Gen {
       uint32_t k = flat_conn_stmt++;
       if (k >= prog.conn_delivers.size() || prog.conn_delivers[k].sub_id != sub)
         throw FilterError("internal: packet-filter statement order");
-      hip += "  cm[" + std::to_string(k / 64) + "] |= " + R + " ? (1ull << " + std::to_string(k % 64) + ") : 0ull;\n";
+      hip += "  RTN_DM_SET(cm, " + std::to_string(k / 64) + ", " + std::to_string(k % 64) + ", " + R + ");\n";
     };
     for (auto& dv : n.deliver) stmt((uint32_t)dv.id);
     for (auto& sv : n.stream) stmt((uint32_t)sv.id);

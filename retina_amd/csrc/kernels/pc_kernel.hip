@@ -3,8 +3,8 @@
 // the RTN_FILTER marker below (the analogue of filtergen's generated `packet_continue`), and the
 // whole translation unit is compiled once per subscription set (hiprtc at rtn_pc_create, or
 // hipcc --genco ahead of time). It holds the packet-stage kernels -- rtn_pc_kernel_s64 for 64-byte
-// slots, rtn_pc_kernel_split for 64-byte head slots + 64-byte ext slots, rtn_pc_kernel for any
-// larger stride (a multiple of 64) -- and rtn_pd_kernel, the PacketDeliver filter (rtn_pd_run),
+// slots, rtn_pc_kernel_split for 64-byte head slots + 64-byte ext slots (rtn_pc_kernel_splitc when
+// the ext rows are compact), rtn_pc_kernel for any larger stride (a multiple of 64) -- and rtn_pd_kernel, the PacketDeliver filter (rtn_pd_run),
 // whose generated tree (RTN_PD_FILTER marker) comes from the same program.
 //
 // Per packet it reproduces, bit for bit:
@@ -94,6 +94,10 @@ struct rtn_view {
 #define rtn_l4_be16(v, off) ((rtn_l4_b(v, off) << 8) | rtn_l4_b(v, (off) + 1))
 #define rtn_l3_be32(v, off) ((rtn_l3_be16(v, off) << 16) | rtn_l3_be16(v, (off) + 2))
 #define rtn_l4_be32(v, off) ((rtn_l4_be16(v, off) << 16) | rtn_l4_be16(v, (off) + 2))
+
+// Statement-mask bit b of word w, set under a node's reach flag r (the generated filters' only
+// form for delivery bits).
+#define RTN_DM_SET(m, w, b, r) ((m)[w] |= (r) ? (1ull << (b)) : 0ull)
 
 //@@RTN_FILTER@@
 
@@ -559,10 +563,12 @@ __device__ __forceinline__ void rtn_group(const rtn_args& a, rtn_u32 g, rtn_u32 
 
 // Chunk loop. Each wave takes chunks wave_g, wave_g + nwaves, ... and walks a chunk's groups in
 // order. MODE: RTN_S64 (64-byte slots), RTN_SPLIT (64-byte slots + ext slab holding bytes
-// 64..127), RTN_MONO (monolithic slots of any stride >= 64).
+// 64..127 of every frame), RTN_SPLITC (the same with compact ext rows, RTN_BATCH_EXT_COMPACT),
+// RTN_MONO (monolithic slots of any stride >= 64).
 #define RTN_S64 0
 #define RTN_SPLIT 1
 #define RTN_MONO 2
+#define RTN_SPLITC 3
 template <int MODE>
 __device__ __forceinline__ void rtn_run(const rtn_args& a) {
   const rtn_u32 lane = threadIdx.x & 63u;
@@ -622,7 +628,7 @@ __device__ __forceinline__ void rtn_run(const rtn_args& a) {
         // number of needing frames of the chunk before this one
         rtn_u64 row = (rtn_u64)g * 64u + lane;
         bool load = need;
-        if (MODE == RTN_SPLIT && (a.flags & 16u)) {
+        if (MODE == RTN_SPLITC) {
           const rtn_u64 nm = __ballot(need);
           row = (rtn_u64)a.ext_chunk[c] + ch.next + (rtn_u32)__popcll(nm & lane_lt);
           ch.next += (rtn_u32)__popcll(nm);
@@ -631,7 +637,7 @@ __device__ __forceinline__ void rtn_run(const rtn_args& a) {
         }
         if (load) {
           // bytes 64..127: the ext slot (split layout) or the slot's second half (monolithic)
-          const rtn_v4u* hi = MODE == RTN_SPLIT
+          const rtn_v4u* hi = MODE != RTN_MONO
                                   ? reinterpret_cast<const rtn_v4u*>(a.ext + row * 64u)
                                   : reinterpret_cast<const rtn_v4u*>(a.slab + (rtn_u64)(g * 64u + lane) * a.stride) + 4;
 #pragma unroll
@@ -685,6 +691,7 @@ __device__ __forceinline__ void rtn_run(const rtn_args& a) {
 extern "C" __global__ void __launch_bounds__(256) rtn_pc_kernel(rtn_args a) { rtn_run<RTN_MONO>(a); }
 extern "C" __global__ void __launch_bounds__(256) rtn_pc_kernel_s64(rtn_args a) { rtn_run<RTN_S64>(a); }
 extern "C" __global__ void __launch_bounds__(256) rtn_pc_kernel_split(rtn_args a) { rtn_run<RTN_SPLIT>(a); }
+extern "C" __global__ void __launch_bounds__(256) rtn_pc_kernel_splitc(rtn_args a) { rtn_run<RTN_SPLITC>(a); }
 
 // ---------------------------------------------------------------------------------------------
 // PacketDeliver filter (rtn_pd_run): the generated `packet_deliver` (filtergen/src/lib.rs:357-362,

@@ -262,6 +262,7 @@ struct rtn_pc {
   hipFunction_t fn = nullptr;        // rtn_pc_kernel: monolithic slots, any stride (multiple of 64)
   hipFunction_t fn_s64 = nullptr;    // rtn_pc_kernel_s64: 64-byte slots
   hipFunction_t fn_split = nullptr;  // rtn_pc_kernel_split: 64-byte slots + ext
+  hipFunction_t fn_splitc = nullptr; // rtn_pc_kernel_splitc: 64-byte slots + compact ext rows
   hipFunction_t fn_pd = nullptr;     // rtn_pd_kernel: the PacketDeliver filter (rtn_pd_run)
   uint32_t blocks = 0;
   // used when the caller passes no counters: word RTN_CNT_STATUS accumulates the status bits of
@@ -460,6 +461,8 @@ int32_t rtn_pc_create_from_program(rtn_program_t* p, int device, rtn_pc_t** out)
   if (e != hipSuccess) return fail(RTN_EDEVICE, std::string("hipModuleGetFunction: ") + hipGetErrorString(e));
   e = hipModuleGetFunction(&pc->fn_split, pc->module, "rtn_pc_kernel_split");
   if (e != hipSuccess) return fail(RTN_EDEVICE, std::string("hipModuleGetFunction: ") + hipGetErrorString(e));
+  e = hipModuleGetFunction(&pc->fn_splitc, pc->module, "rtn_pc_kernel_splitc");
+  if (e != hipSuccess) return fail(RTN_EDEVICE, std::string("hipModuleGetFunction: ") + hipGetErrorString(e));
   e = hipModuleGetFunction(&pc->fn_pd, pc->module, "rtn_pd_kernel");
   if (e != hipSuccess) return fail(RTN_EDEVICE, std::string("hipModuleGetFunction: ") + hipGetErrorString(e));
   e = hipMalloc(&pc->scratch_counters, RTN_COUNTERS_BYTES);
@@ -552,7 +555,8 @@ int32_t rtn_pc_run(rtn_pc_t* pc, const rtn_batch_t* in, rtn_pc_out_t* out, void*
   if (blocks > need) blocks = need;
   if (blocks == 0) blocks = 1;
   void* params[] = {&a};
-  hipFunction_t fn = in->ext ? pc->fn_split : (in->stride == 64 ? pc->fn_s64 : pc->fn);
+  hipFunction_t fn = in->ext ? ((in->flags & RTN_BATCH_EXT_COMPACT) ? pc->fn_splitc : pc->fn_split)
+                             : (in->stride == 64 ? pc->fn_s64 : pc->fn);
   e = hipModuleLaunchKernel(fn, blocks, 1, 1, 256, 1, 1, 0, s, params, nullptr);
   if (e != hipSuccess) return fail(RTN_EDEVICE, std::string("hipModuleLaunchKernel: ") + hipGetErrorString(e));
   return RTN_OK;

@@ -31,7 +31,8 @@ def ceiling(src: str) -> str:
 }'''
     for k in ("rtn_pc_kernel(rtn_args a) { rtn_run<RTN_MONO>(a); }",
               "rtn_pc_kernel_s64(rtn_args a) { rtn_run<RTN_S64>(a); }",
-              "rtn_pc_kernel_split(rtn_args a) { rtn_run<RTN_SPLIT>(a); }"):
+              "rtn_pc_kernel_split(rtn_args a) { rtn_run<RTN_SPLIT>(a); }",
+              "rtn_pc_kernel_splitc(rtn_args a) { rtn_run<RTN_SPLITC>(a); }"):
         src = _sub(src, k, k.split(" {")[0] + " " + body)
     return src
 
@@ -97,7 +98,34 @@ def _store_asm(mods: str):
     return v
 
 
-VARIANTS.update({"dense": dense, "nobitmaps": nobitmaps, "bm128": bm128, "noext": noext, "tstores": tstores,
+def dm_opq(src: str) -> str:
+    """Delivery bits as an opaque 0/1 shifted into its half-word (v_cndmask with inline 0/1, then
+    v_lshl_or with an inline shift): no 1 << b constant held in a register across the loop."""
+    return _sub(src, "#define RTN_DM_SET(m, w, b, r) ((m)[w] |= (r) ? (1ull << (b)) : 0ull)",
+                "__device__ __forceinline__ rtn_u32 rtn_opq(rtn_u32 x) { asm(\"\" : \"+v\"(x)); return x; }\n"
+                "#define RTN_DM_SET(m, w, b, r) ((m)[w] |= (rtn_u64)(rtn_opq((r) ? 1u : 0u) << ((b) % 32u)) << ((b) / 32u * 32u))")
+
+
+def oldform(src: str) -> str:
+    """The compact ext path as a run-time branch of the split kernel instance (round-2 form)."""
+    src = _sub(src, "rtn_pc_kernel_splitc(rtn_args a) { rtn_run<RTN_SPLITC>(a); }",
+               "rtn_pc_kernel_splitc(rtn_args a) { rtn_run<RTN_SPLIT>(a); }")
+    return _sub(src, "        if (MODE == RTN_SPLITC) {\n          const rtn_u64 nm = __ballot(need);",
+                "        if (MODE == RTN_SPLIT && (a.flags & 16u)) {\n          const rtn_u64 nm = __ballot(need);")
+
+
+def splitc_w4(src: str) -> str:
+    """The compact split kernel held to 4 waves per SIMD (<= 128 VGPRs)."""
+    return _sub(src, "extern \"C\" __global__ void __launch_bounds__(256) rtn_pc_kernel_splitc(",
+                "extern \"C\" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) rtn_pc_kernel_splitc(")
+
+
+def splitc_pf(src: str) -> str:
+    """The compact split kernel also keeps the next group's head loads in flight."""
+    return _sub(src, "constexpr bool prefetch = MODE == RTN_S64;", "constexpr bool prefetch = MODE == RTN_S64 || MODE == RTN_SPLITC;")
+
+
+VARIANTS.update({"oldform": oldform, "splitc_w4": splitc_w4, "splitc_pf": splitc_pf, "dm_opq": dm_opq, "dense": dense, "nobitmaps": nobitmaps, "bm128": bm128, "noext": noext, "tstores": tstores,
                  "noconn": noconn, "st_sc1": _store_asm("sc1"), "st_sc0sc1": _store_asm("sc0 sc1"),
                  "st_ntsc1": _store_asm("nt sc1"), "st_nt": _store_asm("nt")})
 
