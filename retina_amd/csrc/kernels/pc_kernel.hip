@@ -592,6 +592,9 @@ __device__ __forceinline__ void rtn_run(const rtn_args& a) {
     const rtn_u32 gb = c * RTN_CHUNK_GROUPS;
     const rtn_u32 ge = gb + RTN_CHUNK_GROUPS < nw ? gb + RTN_CHUNK_GROUPS : nw;
     rtn_chunk ch = {(rtn_u64)c * (64u * RTN_CHUNK_GROUPS), 0u, 0u, 0u, 0u, 0u, 0u, 0ull, 0ull, 0ull};
+    // compact ext: the chunk's first row, read once per chunk (its latency overlaps the first
+    // group's loads; read per group it was a dependent round trip in every group)
+    const rtn_u32 xrow0 = MODE == RTN_SPLITC ? a.ext_chunk[c] : 0u;
     // 64-byte slots without ext: the next group's loads are issued before this group is parsed,
     // so one group of loads is always in flight per wave (cfg2 -2.2 %, in-process A/B; with the
     // split layout's dependent ext loads it measured 5 % slower on cfg4 and is not used there)
@@ -630,7 +633,7 @@ __device__ __forceinline__ void rtn_run(const rtn_args& a) {
         bool load = need;
         if (MODE == RTN_SPLITC) {
           const rtn_u64 nm = __ballot(need);
-          row = (rtn_u64)a.ext_chunk[c] + ch.next + (rtn_u32)__popcll(nm & lane_lt);
+          row = (rtn_u64)xrow0 + ch.next + (rtn_u32)__popcll(nm & lane_lt);
           ch.next += (rtn_u32)__popcll(nm);
           load = need && row < a.ext_rows;
           if (need && !load) acc.status |= 4u;  // RTN_STATUS_EXT_ROWS
