@@ -235,3 +235,47 @@ def test_conn_stage_leaves_other_outputs_alone(gpu):
     a = helpers.gpu_run(SETS["conn"], slab, 128, dlen, conn=True)
     b = helpers.gpu_run(SETS["conn"], slab, 128, dlen, conn=False)
     helpers.assert_same(a, b, "conn on/off")
+
+
+def _random_conn_spec(seed: int) -> str | None:
+    """A random subscription set over CONN_FILTERS x CONN_DTS (as the tree test above draws them),
+    or None when filtergen would reject it."""
+    rng = np.random.default_rng(100 + seed)
+    subs = []
+    for k in range(int(rng.integers(2, 7))):
+        f = CONN_FILTERS[int(rng.integers(0, len(CONN_FILTERS)))]
+        d = CONN_DTS[int(rng.integers(0, len(CONN_DTS)))]
+        stream = ("packets=1",) if rng.random() < 0.1 and d in (["PktCount", "FiveTuple"], ["ConnRecord"]) else ()
+        subs.append((f, d, f"cb{k}", *stream))
+    spec = synth._toml(subs)
+    try:
+        pc.Program.from_spec(spec)
+    except pc.FilterError:
+        return None
+    return spec
+
+
+def test_random_conn_specs_compile():
+    """Most of the GPU test's random sets are valid (the test below is not vacuous)."""
+    assert sum(_random_conn_spec(s) is not None for s in range(12)) >= 8
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(12))
+def test_conn_stage_random_sets(seed, gpu):
+    """The first-packet filter (FilterLayer::Packet), ConnId and creates bits of random
+    subscription sets, bit-exact against the oracle on the adversarial + synthetic corpora, in
+    the monolithic, split and compact split layouts."""
+    spec = _random_conn_spec(seed)
+    if spec is None:
+        pytest.skip("filtergen rejects this random set")
+    s1, d1 = _corpus("adversarial")
+    s2, d2 = _corpus("synth")
+    slab, dlen = np.concatenate([s1, s2]), np.concatenate([d1, d2])
+    layout = ("mono", "split", "compact")[seed % 3]
+    got = helpers.gpu_run(spec, slab, 128, dlen, split=False if layout == "mono" else
+                          ("compact" if layout == "compact" else True), conn=True)
+    hi, cdm = helpers.oracle_conn(spec, slab, 128, dlen, got["fwd"])
+    assert np.array_equal(got["conn"], hi), f"seed {seed} ({layout})"
+    if got["program"].info["conn_words"]:
+        assert np.array_equal(got["cdm"], cdm), f"seed {seed} ({layout})"
