@@ -11,6 +11,7 @@ and the max over ranks is reported. Rank 0 prints one JSON line.
 from __future__ import annotations
 
 import argparse
+import dataclasses
 import json
 import os
 import sys
@@ -263,10 +264,17 @@ def e2e_rate(ctx, slab: np.ndarray, dlen: np.ndarray, stride: int, dev, chunk: i
     h_bm = [torch.empty(bufs[0][4].pc_bitmap.numel() * 2, dtype=torch.uint8).pin_memory() for _ in range(nstreams)]
     h_a6 = [torch.empty(bufs[0][4].addr6.numel(), dtype=torch.uint8).pin_memory() for _ in range(nstreams)] if wide else None
 
-    def one_pass():
+    # zero-copy outputs: the kernel writes records (and IPv6 addresses) straight into pinned host
+    # memory over PCIe, so only what was produced crosses the link (pc.MappedHost)
+    zc_outs = [dataclasses.replace(bufs[k][4], l4=pc.MappedHost(h_out[k]),
+                                   addr6=pc.MappedHost(h_a6[k]) if wide else None) for k in range(nstreams)]
+
+    def one_pass(zero_copy: bool = True):
         for k, (s, m, r0, nr, ch) in enumerate(plan):
             st = streams[k % nstreams]
             d_slab, d_dlen, d_ext, d_chunk, out = bufs[k % nstreams]
+            if zero_copy:
+                out = zc_outs[k % nstreams]
             with torch.cuda.stream(st):
                 d_slab[:m * run_stride].copy_(h_slab[s * run_stride:(s + m) * run_stride], non_blocking=True)
                 d_dlen[:m].copy_(h_dlen[s:s + m], non_blocking=True)
@@ -277,26 +285,49 @@ def e2e_rate(ctx, slab: np.ndarray, dlen: np.ndarray, stride: int, dev, chunk: i
                     ctx.run(d_slab, 64, d_dlen, m, out, stream=st, ext=d_ext[:max(nr, 1) * 64], ext_chunk=d_chunk)
                 else:
                     ctx.run(d_slab, run_stride, d_dlen, m, out, stream=st, dl_le64=dl_le64)
-                h_out[k % nstreams].copy_(out.l4, non_blocking=True)
+                if not zero_copy:
+                    h_out[k % nstreams].copy_(out.l4, non_blocking=True)
+                    if wide:
+                        h_a6[k % nstreams].copy_(out.addr6, non_blocking=True)
                 nb = out.pc_bitmap.numel()
                 h_bm[k % nstreams][:nb].copy_(out.pc_bitmap, non_blocking=True)
                 h_bm[k % nstreams][nb:].copy_(out.fwd_bitmap, non_blocking=True)
-                if wide:
-                    h_a6[k % nstreams].copy_(out.addr6, non_blocking=True)
 
-    one_pass()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    reps = 3
-    for _ in range(reps):
-        one_pass()
-    torch.cuda.synchronize(dev)
-    dt = (time.perf_counter() - t0) / reps
+    def h2d_pass():  # the same host -> HBM copies alone: the link's ceiling for this layout
+        for k, (s, m, r0, nr, ch) in enumerate(plan):
+            d_slab, d_dlen, d_ext, d_chunk, _ = bufs[k % nstreams]
+            with torch.cuda.stream(streams[k % nstreams]):
+                d_slab[:m * run_stride].copy_(h_slab[s * run_stride:(s + m) * run_stride], non_blocking=True)
+                d_dlen[:m].copy_(h_dlen[s:s + m], non_blocking=True)
+                if ch is not None:
+                    if nr:
+                        d_ext[:nr * 64].copy_(h_ext[r0 * 64:(r0 + nr) * 64], non_blocking=True)
+                    d_chunk[:len(ch)].copy_(ch, non_blocking=True)
+
+    def timed(fn, reps=3):
+        fn()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize(dev)
+        return (time.perf_counter() - t0) / reps
+
+    dt = timed(one_pass)
+    dt_copies = timed(lambda: one_pass(zero_copy=False))
+    dt_h2d = timed(h2d_pass)
+    h2d_bytes = n * (run_stride + 2) + (int(h_ext.numel()) if wide and compact else 0)
     layout = "compact split" if wide and compact else f"{run_stride}-B slots"
     return {"mpps": round(n / dt / 1e6, 1), "seconds_per_batch": round(dt, 4), "chunk_frames": chunk,
             "streams": nstreams, "layout": layout,
-            "note": f"pinned host -> HBM copy of the frames ({layout}) + data_len, kernel, D2H of bitmaps, "
-                    "L4 records" + (" and IPv6 addresses" if wide else "") + "; PCIe-bound"}
+            "h2d_only": {"mpps": round(n / dt_h2d / 1e6, 1), "gbs": round(h2d_bytes / dt_h2d / 1e9, 2),
+                         "bytes_per_batch": h2d_bytes},
+            "frac_of_h2d_only": round(dt_h2d / dt, 3),
+            "mpps_with_d2h_copies": round(n / dt_copies / 1e6, 1),
+            "note": f"pinned host -> HBM copy of the frames ({layout}) + data_len, kernel writing the L4 records"
+                    + (" and IPv6 addresses" if wide else "") + " straight into pinned host memory (zero-copy), "
+                    "D2H of the bitmaps; PCIe-bound: h2d_only times the same host -> HBM copies alone; "
+                    "mpps_with_d2h_copies copies the whole record buffers back instead"}
 
 
 # Packet-level subscriptions that match at the protocol/session layer: their packets are

@@ -539,6 +539,35 @@ def pd_replay(pd: dict, counts_row, facts_row) -> list[int]:
     return rec(list(range(len(stmts))), 0)
 
 
+class MappedHost:
+    """A pinned host tensor (torch `pin_memory()`) seen through its device address, for output
+    buffers the kernel writes straight into host memory over PCIe (no D2H copy): the C ABI takes
+    plain pointers, and hipHostGetDevicePointer gives the one the GPU may use. Raises if the
+    memory is not mapped for the device."""
+
+    def __init__(self, host_tensor):
+        if not host_tensor.is_pinned():
+            raise RetinaError(-22, "MappedHost needs a pinned host tensor")
+        hip = C.CDLL("libamdhip64.so")
+        hip.hipHostGetDevicePointer.argtypes = [C.POINTER(C.c_void_p), C.c_void_p, C.c_uint]
+        hip.hipHostGetDevicePointer.restype = C.c_int
+        p = C.c_void_p()
+        rc = hip.hipHostGetDevicePointer(C.byref(p), C.c_void_p(host_tensor.data_ptr()), 0)
+        if rc != 0 or not p.value:
+            raise RetinaError(-19, f"hipHostGetDevicePointer failed ({rc})")
+        self.host = host_tensor
+        self._dptr = int(p.value)
+
+    def data_ptr(self) -> int:
+        return self._dptr
+
+    def numel(self) -> int:
+        return self.host.numel()
+
+    def cpu(self):
+        return self.host
+
+
 def _out_struct(out: PCOutputs) -> _Out:
     ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
     return _Out(ptr(out.pc_bitmap), ptr(out.fwd_bitmap), ptr(out.l4), ptr(out.addr6), ptr(out.dlv_bitmap),

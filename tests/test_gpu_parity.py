@@ -264,3 +264,30 @@ def test_misaligned_record_array_is_einval(gpu):
     ctx.run(d_slab, 64, d_dlen, len(dlen), out)
     torch.cuda.synchronize()
     assert int(out.counters.view(torch.int32)[1]) > 0
+
+
+@pytest.mark.gpu
+def test_outputs_in_mapped_host_memory(gpu):
+    """rtn_pc_run takes plain pointers: records and IPv6 addresses written straight into pinned
+    host memory (pc.MappedHost, the end-to-end path's zero-copy outputs) equal a run into HBM."""
+    import dataclasses
+
+    import torch
+
+    n = (1 << 16) + 77
+    slab, dlen = synth.cfg3(n, start=4242)
+    dev = torch.device("cuda", 0)
+    ctx = pc.PacketContinue(pc.Program.from_spec(SETS["cfg3"]), 0)
+    d_slab = torch.from_numpy(slab).to(dev)
+    d_dlen = torch.from_numpy(dlen.view(np.int16)).to(dev)
+    ref = ctx.run(d_slab, 128, d_dlen, n, ctx.alloc_outputs(n, addr6=True))
+    dev_out = ctx.alloc_outputs(n, addr6=True)
+    mapped = dataclasses.replace(
+        dev_out, l4=pc.MappedHost(torch.zeros(dev_out.l4.numel(), dtype=torch.uint8).pin_memory()),
+        addr6=pc.MappedHost(torch.zeros(dev_out.addr6.numel(), dtype=torch.uint8).pin_memory()))
+    ctx.run(d_slab, 128, d_dlen, n, mapped)
+    torch.cuda.synchronize()
+    a, b = ref.decode(), mapped.decode()
+    assert np.array_equal(a["fwd"], b["fwd"]) and np.array_equal(a["l4"], b["l4"])
+    assert np.array_equal(a["addr6"], b["addr6"])
+    assert int(b["fwd"].sum()) > n // 2
