@@ -227,6 +227,8 @@ size_t rtn_program_source(const rtn_program_t* p, char* buf, size_t cap); /* ful
 /* Statement k of a deliver mask -> subscription index / Payload flag. */
 int32_t rtn_program_deliver_table(const rtn_program_t* p, uint32_t* sub_ids, uint8_t* is_payload,
                                   uint32_t cap);
+/* Statement k's callback name (the subscription's `callback`; 0 if k is out of range). */
+size_t rtn_program_deliver_callback(const rtn_program_t* p, uint32_t k, char* buf, size_t cap);
 /* The packet-level keep/drop filter for the NIC (FilterFactory.filter_str, get_hw_filter in
  * filtergen/src/lib.rs:233-238): the PacketContinue tree's paths joined with "or" ("" = keep all).
  * Installing it as rte_flow rules (core/src/filter/hardware) is the caller's business. */

@@ -70,6 +70,13 @@ def build_library(force: bool = False) -> Path:
         _run(["g++", "-std=c++17", "-O2", "-Wall", "-D__HIP_PLATFORM_AMD__", f"-I{ROOT / 'include'}",
               f"-I{ROCM / 'include'}", str(off_src), "-o", str(off), f"-L{LIB}", "-lretina_pc",
               "-Wl,-rpath,$ORIGIN", f"-L{ROCM / 'lib'}", f"-Wl,-rpath,{ROCM / 'lib'}", "-lamdhip64"])
+    # the C++ Subscription mirror (include/retina_subscription.hpp) driven by its GPU test
+    chk = LIB / "subscription_check"
+    chk_src = ROOT / "tests" / "cpp" / "subscription_check.cpp"
+    if force or _stale(chk, [chk_src, so, ROOT / "include" / "retina_subscription.hpp"] + hdrs):
+        _run(["g++", "-std=c++17", "-O2", "-Wall", "-Wextra", "-D__HIP_PLATFORM_AMD__", f"-I{ROOT / 'include'}",
+              f"-I{ROCM / 'include'}", str(chk_src), "-o", str(chk), f"-L{LIB}", "-lretina_pc",
+              "-Wl,-rpath,$ORIGIN", f"-L{ROCM / 'lib'}", f"-Wl,-rpath,{ROCM / 'lib'}", "-lamdhip64"])
     cli = LIB / "rtnc"
     main = CSRC / "filtergen" / "rtnc_main.cpp"
     if force or _stale(cli, fg + [main] + hdrs):

@@ -430,6 +430,11 @@ int32_t rtn_program_deliver_table(const rtn_program_t* p, uint32_t* sub_ids, uin
   return RTN_OK;
 }
 
+size_t rtn_program_deliver_callback(const rtn_program_t* p, uint32_t k, char* buf, size_t cap) {
+  if (!p || k >= p->prog.delivers.size()) return 0;
+  return copy_text(p->prog.delivers[k].callback, buf, cap);
+}
+
 int32_t rtn_program_code_object(rtn_program_t* p, const uint8_t** data, size_t* len) {
   if (!p || !data || !len) return fail(RTN_EINVAL, "null argument");
   if (!p->code) {

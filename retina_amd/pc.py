@@ -69,6 +69,7 @@ EXPORTS = {
     "rtn_program_rust": (C.c_size_t, [C.c_void_p, C.c_char_p, C.c_size_t]),
     "rtn_program_source": (C.c_size_t, [C.c_void_p, C.c_char_p, C.c_size_t]),
     "rtn_program_deliver_table": (C.c_int32, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32]),
+    "rtn_program_deliver_callback": (C.c_size_t, [C.c_void_p, C.c_uint32, C.c_char_p, C.c_size_t]),
     "rtn_program_hw_filter": (C.c_size_t, [C.c_void_p, C.c_char_p, C.c_size_t]),
     "rtn_program_conn_tree": (C.c_size_t, [C.c_void_p, C.c_char_p, C.c_size_t]),
     "rtn_program_conn_rust": (C.c_size_t, [C.c_void_p, C.c_char_p, C.c_size_t]),
@@ -213,6 +214,16 @@ class Program:
     @property
     def source(self) -> str:
         return _text(lib().rtn_program_source, self._h)
+
+    def deliver_callbacks(self) -> list[str]:
+        """Callback name of every packet-level statement, in statement order."""
+        out = []
+        for k in range(self.info["n_deliver_stmts"]):
+            m = lib().rtn_program_deliver_callback(self._h, k, None, 0)
+            buf = C.create_string_buffer(m + 1)
+            lib().rtn_program_deliver_callback(self._h, k, buf, m + 1)
+            out.append(buf.value.decode())
+        return out
 
     def deliver_table(self) -> tuple[np.ndarray, np.ndarray]:
         n = self.info["n_deliver_stmts"]

@@ -106,8 +106,8 @@ class Subscription:
         self.device = device
         self.stats = {k: 0 for k in STAT_NAMES}
         subs, pay = self.program.deliver_table()
-        names = _callbacks(spec)
-        self.callback_sites = [(int(s), names[int(s)], "Payload" if p else "ZcFrame") for s, p in zip(subs, pay)]
+        names = self.program.deliver_callbacks()
+        self.callback_sites = [(int(s), cb, "Payload" if p else "ZcFrame") for s, p, cb in zip(subs, pay, names)]
 
     def run(self, slab, stride: int, data_len, n: int | None = None, ext=None, stream=None,
             core_id: int = 0) -> Burst:
@@ -128,10 +128,3 @@ class Subscription:
             self.stats[k] += v
         return b
 
-
-def _callbacks(spec: str) -> list[str]:
-    try:
-        import tomllib
-    except ImportError:  # python < 3.11
-        import tomli as tomllib
-    return [s["callback"] for s in tomllib.loads(spec).get("subscriptions", [])]

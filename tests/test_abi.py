@@ -234,3 +234,17 @@ def test_ext_needed_rule_matches_header(tmp_path):
     head, ext, chunk = pc.split_slab(slab.reshape(-1), 128, dlen, compact=True)
     assert ext.size == 64 * int(py_rule.sum()) and chunk[0] == 0 and len(chunk) == (len(dlen) + 511) // 512
     assert np.array_equal(ext.reshape(-1, 64), slab[py_rule, 64:128])
+
+
+def test_deliver_callbacks_name_each_statement():
+    """rtn_program_deliver_callback: statement k's callback is its subscription's (the C++ and
+    Python Subscription mirrors read callback names through it); out of range gives 0."""
+    from golden.filter_sets import SETS
+    from oracle import filterlang
+
+    for fset in ("payload", "cfg4", "quirks"):
+        prog = pc.Program.from_spec(SETS[fset])
+        subs, _ = prog.deliver_table()
+        cbs = [s.callback for s in filterlang.load_spec(SETS[fset])]
+        assert prog.deliver_callbacks() == [cbs[int(s)] for s in subs]
+        assert pc.lib().rtn_program_deliver_callback(prog._h, prog.info["n_deliver_stmts"], None, 0) == 0

@@ -65,3 +65,63 @@ def test_subscription_mirror(fset, gpu):
             want_calls = [(st[k][0], subs[st[k][0]].callback, st[k][1]) for k in fired]
             assert cb.get(i, []) == want_calls, i
     assert sub.stats == totals
+
+
+CHECK = Path(__file__).resolve().parent.parent / "retina_amd" / "_lib" / "subscription_check"
+
+
+def _run_cpp(spec: str, slab: np.ndarray, dlen: np.ndarray, tmp_path) -> dict:
+    """tests/cpp/subscription_check.cpp (include/retina_subscription.hpp) on one burst."""
+    import subprocess
+
+    (tmp_path / "spec.toml").write_text(spec)
+    (tmp_path / "slab.bin").write_bytes(np.ascontiguousarray(slab, np.uint8).tobytes())
+    (tmp_path / "dlen.bin").write_bytes(np.ascontiguousarray(dlen, np.uint16).tobytes())
+    r = subprocess.run([str(CHECK), str(tmp_path / "spec.toml"), str(tmp_path / "slab.bin"), str(tmp_path / "dlen.bin")],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    out = {"pc": [], "l4": [], "cb": [], "stat": {}}
+    for line in r.stdout.splitlines():
+        f = line.split()
+        if f[0] == "pc":
+            out["pc"].append(int(f[1]))
+        elif f[0] == "l4":
+            out["l4"].append(f[1:])
+        elif f[0] == "cb":
+            out["cb"].append((int(f[1]), int(f[2]), f[3], f[4]))
+        else:
+            out["stat"][f[1]] = int(f[2])
+    return out
+
+
+@pytest.mark.parametrize("fset", ["payload", "cfg4", "quirks"])
+def test_cpp_subscription_mirror(fset, gpu, tmp_path):
+    """The C++ mirror (include/retina_subscription.hpp) over the C ABI: continue_packet,
+    process_packet's L4Contexts, the packet-level callbacks in call order and the stats, each
+    equal to the oracle on the traces + adversarial corpus."""
+    t = np.load(GOLD / "traces.npz")
+    a = np.load(GOLD / "corpus_adversarial.npz")
+    slab, dlen = np.concatenate([t["slab"], a["slab"]]), np.concatenate([t["dlen"], a["dlen"]])
+    spec = SETS[fset]
+    got = _run_cpp(spec, slab, dlen, tmp_path)
+    r, want_stats = _expected_stats(spec, slab, dlen)
+    assert got["stat"] == want_stats
+    assert got["pc"] == list(np.nonzero(r["pc"])[0])
+    assert [int(x[0]) for x in got["l4"]] == list(r["rec"]["idx"])
+    for g, x in zip(got["l4"], r["rec"]):
+        v6 = "." not in g[1]
+        src = bytes.fromhex(g[1]) if v6 else bytes(int(b) for b in g[1].split("."))
+        dst = bytes.fromhex(g[3]) if v6 else bytes(int(b) for b in g[3].split("."))
+        w = len(src)
+        assert (src + bytes(16 - w), dst + bytes(16 - w)) == (bytes(x["src"]), bytes(x["dst"]))
+        assert [int(v) for v in (g[2], g[4], g[5], g[6], g[7], g[8], g[9], g[10])] == \
+            [x["sport"], x["dport"], x["proto"], x["offset"], x["length"], x["seq"], x["ack"], x["flags"]]
+    tree = filterlang.PacketTree(filterlang.load_spec(spec))
+    st = packet.statement_table(tree)
+    subs = filterlang.load_spec(spec)
+    rows = slab.reshape(-1, 128)
+    want_cb = []
+    for i in range(len(dlen)):
+        _, fired = packet.evaluate(tree, rows[i].tobytes(), int(dlen[i]))
+        want_cb += [(i, st[k][0], subs[st[k][0]].callback, st[k][1]) for k in fired]
+    assert got["cb"] == want_cb
