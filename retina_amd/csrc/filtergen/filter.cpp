@@ -138,6 +138,18 @@ void flat_patterns(const FlatNode& n, std::vector<Predicate>& preds, std::vector
 }
 }  // namespace
 
+// FlatPTree::new + prune_branches + to_flat_patterns (ptree_flat.rs:91-174, 257-267)
+std::vector<FlatPattern> flat_ptree_pruned(const std::vector<FlatPattern>& patterns) {
+  FlatNode root{Predicate::unary("ethernet"), false, {}};
+  for (auto& f : patterns) flat_add(root, f);
+  if (root.children.empty()) root.is_terminal = true;
+  flat_prune(root);
+  std::vector<FlatPattern> pruned;
+  std::vector<Predicate> preds;
+  flat_patterns(root, preds, pruned);
+  return pruned;
+}
+
 // core/src/filter/mod.rs:113-139
 Filter Filter::make(const std::string& filter_raw) {
   auto raw = parse_filter_raw(filter_raw);
@@ -151,14 +163,7 @@ Filter Filter::make(const std::string& filter_raw) {
   std::sort(flat.begin(), flat.end());
   flat.erase(std::unique(flat.begin(), flat.end()), flat.end());
 
-  FlatNode root{Predicate::unary("ethernet"), false, {}};
-  for (auto& f : flat) flat_add(root, f);
-  if (root.children.empty()) root.is_terminal = true;
-  flat_prune(root);
-  std::vector<FlatPattern> pruned;
-  std::vector<Predicate> preds;
-  flat_patterns(root, preds, pruned);
-
+  auto pruned = flat_ptree_pruned(flat);
   Filter f;
   for (auto& p : pruned) {
     auto v = to_fully_qualified(p);

@@ -40,6 +40,8 @@ struct LayeredPattern {
 };
 
 std::vector<LayeredPattern> to_fully_qualified(const FlatPattern& p);
+// FlatPTree::new(patterns) + prune_branches + to_flat_patterns (ptree_flat.rs:91-174, 257-267)
+std::vector<FlatPattern> flat_ptree_pruned(const std::vector<FlatPattern>& patterns);
 
 // Filter::new (core/src/filter/mod.rs:113-139)
 struct Filter {

@@ -2,6 +2,7 @@
 // load it and launch it. See include/retina_pc.h for the contract and reference map.
 #include "retina_pc.h"
 #include "retina_ct.h"
+#include "retina_hw.h"
 #include "retina_pd.h"
 
 #include <hip/hip_runtime.h>
@@ -346,6 +347,11 @@ int32_t rtn_program_info(const rtn_program_t* p, rtn_program_info_t* info) {
 
 size_t rtn_program_hw_filter(const rtn_program_t* p, char* buf, size_t cap) {
   return p ? copy_text(p->prog.hw_filter, buf, cap) : 0;
+}
+int32_t rtn_program_hw_rules(const rtn_program_t* p, rtn_flow_validate_fn validate, void* user,
+                             rtn_flow_rule_t* rules, uint32_t cap, uint32_t* n_rules) {
+  if (!p) return fail(RTN_EINVAL, "null program");
+  return rtn_hw_rules(p->prog.hw_filter.c_str(), validate, user, rules, cap, n_rules);
 }
 size_t rtn_program_conn_tree(const rtn_program_t* p, char* buf, size_t cap) {
   return p ? copy_text(p->prog.conn_tree.pprint(), buf, cap) : 0;

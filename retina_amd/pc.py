@@ -60,6 +60,18 @@ class _Info(C.Structure):
                 ("n_pd_facts", C.c_uint32), ("pd_tree_size", C.c_uint32)]
 
 
+class _FlowItem(C.Structure):
+    _fields_ = [("item_type", C.c_uint32), ("size", C.c_uint32), ("spec", C.c_uint8 * 40), ("mask", C.c_uint8 * 40)]
+
+
+class _FlowRule(C.Structure):
+    _fields_ = [("group", C.c_uint32), ("priority", C.c_uint32), ("action", C.c_uint32),
+                ("jump_group", C.c_uint32), ("pattern", C.c_uint32), ("n_items", C.c_uint32),
+                ("items", _FlowItem * 4)]
+
+
+_FLOW_VALIDATE = C.CFUNCTYPE(C.c_int32, C.c_void_p, C.POINTER(_FlowRule))
+
 EXPORTS = {
     "rtn_last_error": (C.c_char_p, []),
     "rtn_program_compile": (C.c_int32, [C.c_char_p, C.c_size_t, C.POINTER(C.c_void_p)]),
@@ -106,6 +118,12 @@ EXPORTS = {
     "rtn_out_pd_counts_bytes": (C.c_size_t, [C.c_uint32, C.c_uint32]),
     "rtn_program_pd_replay": (C.c_int32, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
                                           C.POINTER(C.c_uint32)]),
+    # include/retina_hw.h
+    "rtn_hw_rules": (C.c_int32, [C.c_char_p, _FLOW_VALIDATE, C.c_void_p, C.POINTER(_FlowRule), C.c_uint32,
+                                 C.POINTER(C.c_uint32)]),
+    "rtn_program_hw_rules": (C.c_int32, [C.c_void_p, _FLOW_VALIDATE, C.c_void_p, C.POINTER(_FlowRule),
+                                         C.c_uint32, C.POINTER(C.c_uint32)]),
+    "rtn_hw_patterns": (C.c_size_t, [C.c_char_p, _FLOW_VALIDATE, C.c_void_p, C.c_char_p, C.c_size_t]),
     # include/retina_ingest.h
     "rtn_pcap_open": (C.c_int32, [C.c_char_p, C.c_uint32, C.POINTER(C.c_void_p)]),
     "rtn_pcap_next_batch": (C.c_int32, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint32,
@@ -753,3 +771,45 @@ class PcapReader:
         if not slabs:
             return np.zeros(0, np.uint8), np.zeros(0, np.uint16)
         return np.concatenate(slabs), np.concatenate(lens)
+
+
+# ----------------------------------------------------------------------------------------------
+# Hardware-assist filter (include/retina_hw.h): the rte_flow rules Retina installs on each port.
+
+def _rule_dict(r: "_FlowRule") -> dict:
+    items = [(it.item_type, it.size, bytes(it.spec), bytes(it.mask)) for it in r.items[:r.n_items]]
+    return {"group": r.group, "priority": r.priority, "action": r.action, "jump_group": r.jump_group,
+            "pattern": r.pattern, "items": items}
+
+
+def _validator(validate):
+    """A Python device model (rule dict -> bool) as an rtn_flow_validate_fn (NULL for None)."""
+    if validate is None:
+        return _FLOW_VALIDATE()
+    return _FLOW_VALIDATE(lambda _user, rule: 1 if validate(_rule_dict(rule.contents)) else 0)
+
+
+def hw_rules(filter_str: str | None = None, validate=None, program: "Program | None" = None) -> list[dict]:
+    """rtn_hw_rules / rtn_program_hw_rules: rules as dicts {group, priority, action, jump_group,
+    pattern, items: [(type, size, spec, mask)]}; `validate` models rte_flow_validate."""
+    cb = _validator(validate)
+    n = C.c_uint32(0)
+    L = lib()
+    call = (lambda buf, cap: L.rtn_program_hw_rules(program._h, cb, None, buf, cap, C.byref(n))) if program \
+        else (lambda buf, cap: L.rtn_hw_rules(filter_str.encode(), cb, None, buf, cap, C.byref(n)))
+    rc = call(None, 0)
+    if rc not in (RTN_OK, -34):
+        _check(rc)
+    buf = (_FlowRule * max(n.value, 1))()
+    _check(call(buf, n.value))
+    return [_rule_dict(buf[k]) for k in range(n.value)]
+
+
+def hw_patterns(filter_str: str, validate=None) -> str:
+    """HardwareFilter's patterns, one flat pattern per line (rtn_hw_patterns)."""
+    cb = _validator(validate)
+    L = lib()
+    need = L.rtn_hw_patterns(filter_str.encode(), cb, None, None, 0)
+    buf = C.create_string_buffer(need + 1)
+    L.rtn_hw_patterns(filter_str.encode(), cb, None, buf, need + 1)
+    return buf.value.decode()

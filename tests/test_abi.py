@@ -134,7 +134,19 @@ def test_rec_index_macro_matches_host_decoder(tmp_path):
 _RUST_C = {"u8": "uint8_t", "u16": "uint16_t", "u32": "uint32_t", "u64": "uint64_t", "i32": "int32_t",
            "usize": "size_t"}
 _RUST_TO_HEADER = {"RtnBatch": "rtn_batch_t", "RtnPcOut": "rtn_pc_out_t", "RtnL4Ctx": "rtn_l4ctx_t",
-                   "RtnConn": "rtn_conn_t", "RtnProgramInfo": "rtn_program_info_t"}
+                   "RtnConn": "rtn_conn_t", "RtnProgramInfo": "rtn_program_info_t",
+                   "RtnFlowItem": "rtn_flow_item_t", "RtnFlowRule": "rtn_flow_rule_t"}
+
+
+def _c_decl(t: str, f: str) -> str:
+    """A Rust field type as a C declaration (scalars, raw pointers, [T; N] arrays)."""
+    import re
+
+    m = re.fullmatch(r"\[(\w+);\s*(\d+)\]", t)
+    if m:
+        inner = _RUST_C.get(m.group(1)) or f"twin_{m.group(1)}"
+        return f"{inner} {f}[{m.group(2)}]"
+    return f"{'void*' if t.startswith('*') else _RUST_C[t]} {f}"
 
 
 def _rust_structs(text: str) -> dict:
@@ -159,11 +171,11 @@ def test_integration_rust_structs_match_header(tmp_path):
     text = (Path(__file__).resolve().parent.parent / "INTEGRATION.md").read_text()
     structs = _rust_structs(text)
     assert set(_RUST_TO_HEADER) <= set(structs), sorted(structs)
-    src = '#include "retina_pc.h"\n#include <stddef.h>\n#include <stdint.h>\n'
+    src = '#include "retina_pc.h"\n#include "retina_hw.h"\n#include <stddef.h>\n#include <stdint.h>\n'
     for name, cname in _RUST_TO_HEADER.items():
         src += f"typedef struct {{\n"
         for f, t in structs[name]:
-            src += f"  {'void*' if t.startswith('*') else _RUST_C[t]} {f};\n"
+            src += f"  {_c_decl(t, f)};\n"
         src += f"}} twin_{name};\n"
         src += f"_Static_assert(sizeof(twin_{name}) == sizeof({cname}), \"size of {name}\");\n"
         for f, _ in structs[name]:
@@ -178,10 +190,10 @@ def test_integration_rust_structs_match_header(tmp_path):
     # every field of the C structs is in the twin (no field missing at the end either)
     import re
 
-    hdr = (inc / "retina_pc.h").read_text()
+    hdr = (inc / "retina_pc.h").read_text() + (inc / "retina_hw.h").read_text()
     for name, cname in _RUST_TO_HEADER.items():
         body = re.search(r"typedef struct \w+ \{([^{}]*)\} " + cname + ";", hdr).group(1)
-        cfields = re.findall(r"^\s*[\w\s\*]+?\b(\w+);", re.sub(r"/\*.*?\*/", "", body, flags=re.S), re.M)
+        cfields = re.findall(r"^\s*[\w\s\*]+?\b(\w+)(?:\[\w+\])?;", re.sub(r"/\*.*?\*/", "", body, flags=re.S), re.M)
         assert cfields == [f for f, _ in structs[name]], (name, cfields)
 
 
