@@ -17,6 +17,7 @@ ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0]
 
 FILTERGEN_SRCS = ["ast.cpp", "parser.cpp", "filter.cpp", "ptree.cpp", "codegen.cpp", "hwfilter.cpp"]
 SO_NAME = "libretina_pc.so"
+RUNTIME_SRCS = ["runtime/rtn_runtime.cpp", "runtime/rtn_hw.cpp", "ingest/pcap_ingest.cpp"]
 
 
 def _run(cmd: list[str], cwd: Path | None = None) -> None:
@@ -51,7 +52,7 @@ def build_library(force: bool = False) -> Path:
     inc = _gen_kernel_inc()
     inc_ct = _gen_kernel_inc("ct_kernel", "kCtKernelSrc")
     fg = [CSRC / "filtergen" / s for s in FILTERGEN_SRCS]
-    rt = [CSRC / "runtime" / "rtn_runtime.cpp", CSRC / "runtime" / "rtn_hw.cpp", CSRC / "ingest" / "pcap_ingest.cpp"]
+    rt = [CSRC / s for s in RUNTIME_SRCS]
     hdrs = (list((CSRC / "filtergen").glob("*.hpp")) + list((CSRC / "runtime").glob("*.hpp"))
             + list((ROOT / "include").glob("*.h")) + [inc, inc_ct])
     so = LIB / SO_NAME

@@ -563,7 +563,9 @@ int32_t rtn_pc_run(rtn_pc_t* pc, const rtn_batch_t* in, rtn_pc_out_t* out, void*
   // out blocks as earlier ones retire, which balances the tail better than a persistent grid
   const uint32_t need = (chunks + 3u) / 4u;
   uint32_t blocks = pc->blocks ? pc->blocks : need;
+#ifndef RTN_EXPERIMENTS
   if (blocks > need) blocks = need;
+#endif
   if (blocks == 0) blocks = 1;
   void* params[] = {&a};
   hipFunction_t fn = in->ext ? ((in->flags & RTN_BATCH_EXT_COMPACT) ? pc->fn_splitc : pc->fn_split)

@@ -130,6 +130,16 @@ VARIANTS.update({"oldform": oldform, "splitc_w4": splitc_w4, "splitc_pf": splitc
                  "st_ntsc1": _store_asm("nt sc1"), "st_nt": _store_asm("nt")})
 
 
+def chunk256(src: str) -> str:
+    """Timing only: 256-frame chunks (one wave per chunk, half the work unit; outputs are laid out
+    by 256-frame chunks, so only the plain split layout and 64-B slots apply). Run with @GRID =
+    ceil(n / 1024) blocks so that every chunk still gets its own wave."""
+    return _sub(src, "#define RTN_CHUNK_GROUPS 8u", "#define RTN_CHUNK_GROUPS 4u")
+
+
+VARIANTS["chunk256"] = chunk256
+
+
 def write(name: str, outdir: Path) -> Path:
     """A variant file: a '+'-joined list of VARIANTS applied to the current kernel, or
     'file=<path>' (a kernel source as is, e.g. an older revision: git show REV:path > file)."""
