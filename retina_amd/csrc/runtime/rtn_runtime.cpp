@@ -266,6 +266,7 @@ struct rtn_pc {
   hipFunction_t fn_splitc = nullptr; // rtn_pc_kernel_splitc: 64-byte slots + compact ext rows
   hipFunction_t fn_pd = nullptr;     // rtn_pd_kernel: the PacketDeliver filter (rtn_pd_run)
   uint32_t blocks = 0;
+  uint32_t threads = 256;  // threads per block of the packet kernel (4 waves, one chunk each)
   // used when the caller passes no counters: word RTN_CNT_STATUS accumulates the status bits of
   // such runs until rtn_pc_take_status reads and clears them (the other words are never read)
   uint32_t* scratch_counters = nullptr;
@@ -482,6 +483,7 @@ int32_t rtn_pc_create_from_program(rtn_program_t* p, int device, rtn_pc_t** out)
   if (e != hipSuccess) return fail(RTN_EDEVICE, std::string("hipMemset: ") + hipGetErrorString(e));
 #ifdef RTN_EXPERIMENTS
   if (const char* g = getenv("RTN_GRID")) pc->blocks = (uint32_t)strtoul(g, nullptr, 10);
+  if (const char* b = getenv("RTN_BLOCK")) pc->threads = (uint32_t)strtoul(b, nullptr, 10);
 #endif
   *out = pc.release();
   return RTN_OK;
@@ -561,7 +563,8 @@ int32_t rtn_pc_run(rtn_pc_t* pc, const rtn_batch_t* in, rtn_pc_out_t* out, void*
   const uint32_t chunks = (in->n + RTN_CHUNK_FRAMES - 1u) / RTN_CHUNK_FRAMES;
   // default: one wave per chunk (4 chunks per 256-thread block); the hardware dispatcher hands
   // out blocks as earlier ones retire, which balances the tail better than a persistent grid
-  const uint32_t need = (chunks + 3u) / 4u;
+  const uint32_t threads = pc->threads;
+  const uint32_t need = (chunks + threads / 64u - 1u) / (threads / 64u);
   uint32_t blocks = pc->blocks ? pc->blocks : need;
 #ifndef RTN_EXPERIMENTS
   if (blocks > need) blocks = need;
@@ -570,7 +573,7 @@ int32_t rtn_pc_run(rtn_pc_t* pc, const rtn_batch_t* in, rtn_pc_out_t* out, void*
   void* params[] = {&a};
   hipFunction_t fn = in->ext ? ((in->flags & RTN_BATCH_EXT_COMPACT) ? pc->fn_splitc : pc->fn_split)
                              : (in->stride == 64 ? pc->fn_s64 : pc->fn);
-  e = hipModuleLaunchKernel(fn, blocks, 1, 1, 256, 1, 1, 0, s, params, nullptr);
+  e = hipModuleLaunchKernel(fn, blocks, 1, 1, threads, 1, 1, 0, s, params, nullptr);
   if (e != hipSuccess) return fail(RTN_EDEVICE, std::string("hipModuleLaunchKernel: ") + hipGetErrorString(e));
   return RTN_OK;
 }

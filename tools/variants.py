@@ -137,7 +137,25 @@ def chunk256(src: str) -> str:
     return _sub(src, "#define RTN_CHUNK_GROUPS 8u", "#define RTN_CHUNK_GROUPS 4u")
 
 
-VARIANTS["chunk256"] = chunk256
+def chunk128(src: str) -> str:
+    """Timing only: 128-frame chunks (@GRID = ceil(n / 512) blocks)."""
+    return _sub(src, "#define RTN_CHUNK_GROUPS 8u", "#define RTN_CHUNK_GROUPS 2u")
+
+
+def rb128(src: str) -> str:
+    """Timing only: 128-record blocks (a 512-frame chunk's records in 4 interleaved streams)."""
+    return _sub(src, "#define RTN_RB 64u", "#define RTN_RB 128u")
+
+
+def wpb2(src: str) -> str:
+    """Per-block LDS sized for 2 waves (run with RTN_BLOCK=128: 128-thread blocks, one chunk per
+    wave as before, so a block retires after 2 chunks instead of 4)."""
+    for arr in ("rtn_ring[4]", "rtn_cring[4]", "rtn_ring6[4]", "rtn_tile[4]"):
+        src = _sub(src, arr, arr.replace("[4]", "[2]"))
+    return src
+
+
+VARIANTS.update({"chunk256": chunk256, "chunk128": chunk128, "rb128": rb128, "wpb2": wpb2})
 
 
 def write(name: str, outdir: Path) -> Path:
