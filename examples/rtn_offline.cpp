@@ -73,7 +73,7 @@ constexpr uint64_t kStride = 128;  // every header the parse can reach (98 B max
 struct HostSet {  // one batch in flight: pinned input and result buffers
   uint8_t* slab;        // 128-B slots (mono) or 64-B head slots (compact)
   uint8_t* ext;         // compact: ext rows
-  uint32_t* ext_chunk;  // compact: first row of each 512-frame chunk
+  uint32_t* ext_chunk;  // compact: first row of each RTN_CHUNK_FRAMES-frame chunk
   uint32_t rows = 0;
   uint16_t* dlen;
   uint64_t* fwd;

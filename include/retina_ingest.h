@@ -40,8 +40,8 @@ int32_t rtn_pcap_next_batch(rtn_pcap_t* p, uint8_t* slab, uint64_t stride, uint1
                             uint32_t* n);
 /* The same in the compact split layout (retina_pc.h, RTN_BATCH_EXT_COMPACT): head slot k (64 B)
  * receives the first min(data_len, 64) bytes; a frame for which rtn_ext_needed() holds also gets
- * the next ext row (its bytes [64, 128)); ext_chunk[c] receives the first row of 512-frame chunk c
- * (ceil(cap / 512) entries). *rows = rows written. The batch ends early, at a frame, when ext_cap
+ * the next ext row (its bytes [64, 128)); ext_chunk[c] receives the first row of chunk c (RTN_CHUNK_FRAMES)
+ * (ceil(cap / RTN_CHUNK_FRAMES) entries). *rows = rows written. The batch ends early, at a frame, when ext_cap
  * rows are used (allocate cap rows to never end early). */
 int32_t rtn_pcap_next_batch_split(rtn_pcap_t* p, uint8_t* head, uint8_t* ext, uint32_t ext_cap, uint32_t* ext_chunk,
                                   uint16_t* data_len, uint32_t cap, uint32_t* n, uint32_t* rows);

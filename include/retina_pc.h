@@ -127,8 +127,8 @@ typedef struct rtn_batch {
   const uint8_t* ext;       /* split layout: bytes [64, 128) of each frame, 64-byte slots */
   uint32_t flags;           /* RTN_BATCH_*                                                */
   uint32_t ext_rows;        /* RTN_BATCH_EXT_COMPACT: rows in ext                         */
-  const uint32_t* ext_chunk; /* RTN_BATCH_EXT_COMPACT: [ceil(n/512)] row of the first frame of
-                                each 512-frame chunk that needs one (an exclusive prefix sum) */
+  const uint32_t* ext_chunk; /* RTN_BATCH_EXT_COMPACT: [ceil(n/256)] row of the first frame of
+                                each 256-frame chunk that needs one (an exclusive prefix sum) */
 } rtn_batch_t;
 
 /* The compact split layout (RTN_BATCH_EXT_COMPACT): ext holds bytes [64, 128) only of the frames
@@ -158,7 +158,7 @@ static inline int rtn_ext_needed(const uint8_t* head, uint16_t data_len) {
  * The j-th forwarded IPv6 frame of chunk c (records with RTN_L4_IPV6) has its addresses at
  * addr6[c * RTN_CHUNK_FRAMES + j]; dlv_records are ranked by dlv_bitmap the same way (dense per
  * chunk). Bitmaps hold bit i % 64 of word i / 64. */
-#define RTN_CHUNK_FRAMES 512u
+#define RTN_CHUNK_FRAMES 256u
 #define RTN_REC_BLOCK 64u
 #define RTN_REC_INDEX(n, chunk, k)                                                             \
   (((uint64_t)((k) / RTN_REC_BLOCK) * (((uint64_t)(n) + RTN_CHUNK_FRAMES - 1u) / RTN_CHUNK_FRAMES) + \
@@ -167,15 +167,15 @@ static inline int rtn_ext_needed(const uint8_t* head, uint16_t data_len) {
 typedef struct rtn_pc_out {
   uint64_t* pc_bitmap;   /* [ceil(n/64)]  Actions.data contains PacketContinue               */
   uint64_t* fwd_bitmap;  /* [ceil(n/64)]  ... and L4Context::new succeeded (goes to conntrack) */
-  rtn_l4ctx_t* l4;       /* [ceil(n/512)*512] (rtn_out_l4_bytes) at RTN_REC_INDEX; unused slots undefined */
-  uint8_t* addr6;        /* optional [ceil(n/512)*512][32]: src|dst of the IPv6 records   */
+  rtn_l4ctx_t* l4;       /* [ceil(n/256)*256] (rtn_out_l4_bytes) at RTN_REC_INDEX; unused slots undefined */
+  uint8_t* addr6;        /* optional [ceil(n/256)*256][32]: src|dst of the IPv6 records   */
   uint64_t* dlv_bitmap;  /* [ceil(n/64)] frames with >= 1 packet-level callback (if any)     */
-  uint64_t* dlv_records; /* [ceil(n/512)*512][deliver_words]: statement mask; the frame is the
+  uint64_t* dlv_records; /* [ceil(n/256)*256][deliver_words]: statement mask; the frame is the
                           record's rank among its chunk's dlv_bitmap bits (as for l4)        */
   uint32_t* counters;    /* optional [16] (RTN_COUNTERS_BYTES = 64 B, 8-B aligned), zeroed per run
                           (NULL: no totals, no memset -- one kernel launch); RTN_CNT_* below */
-  rtn_conn_t* conn;      /* optional [ceil(n/512)*512]: connection stage, indexed like l4       */
-  uint64_t* conn_dlv;    /* [ceil(n/512)*512][conn_words] first-packet statement masks; required
+  rtn_conn_t* conn;      /* optional [ceil(n/256)*256]: connection stage, indexed like l4       */
+  uint64_t* conn_dlv;    /* [ceil(n/256)*256][conn_words] first-packet statement masks; required
                           with conn when the program has first-packet statements           */
 } rtn_pc_out_t;
 

@@ -20,7 +20,7 @@
 //                  (CAS on the tag), then lower the slot's `first` to their frame index.
 //   rtn_ct_lookup  every forwarded frame finds its key (tags, then the whole key, so a 64-bit
 //                  fingerprint collision is reported instead of aliasing) and gets its status.
-// A block walks one 512-frame chunk, a wave one group: lane = frame, records ranked by the fwd
+// A block walks one 256-frame chunk, a wave one group: lane = frame, records ranked by the fwd
 // bitmap exactly as rtn_pc_run wrote them.
 #ifndef __HIPCC_RTC__
 #include <hip/hip_runtime.h>
@@ -29,7 +29,8 @@
 typedef unsigned int rtn_u32;
 typedef unsigned long long rtn_u64;
 
-#define RTN_CT_CHUNK 512u   // RTN_CHUNK_FRAMES
+#define RTN_CT_CHUNK 256u   // RTN_CHUNK_FRAMES
+#define RTN_CT_GROUPS (RTN_CT_CHUNK / 64u)
 #define RTN_CT_MAXPROBE 256u
 #define RTN_CT_EMPTY 0ull
 #define RTN_CT_REMOVED 1ull
@@ -145,9 +146,9 @@ __device__ __forceinline__ rtn_u64* rtn_ct_tag(const rtn_ct_args& a, rtn_u32 slo
 #endif
 #define RTN_CT_BLOCK (64u * (RTN_CT_CHUNK / 64u) / RTN_CT_GPW)
 
-// One block per 512-frame chunk; each wave takes RTN_CT_GPW groups and issues all of their loads
+// One block per chunk; each wave takes RTN_CT_GPW groups and issues all of their loads
 // before using any (the walk is latency-bound: a wave per group left too few loads in flight).
-// The record rank comes from the chunk's 8 bitmap words; the IPv6 rank needs the IPv6 counts of
+// The record rank comes from the chunk's RTN_CT_GROUPS bitmap words; the IPv6 rank needs the IPv6 counts of
 // the earlier groups, exchanged through LDS. fn(lane has a record, record index, frame index,
 // record words, rtn_conn_t, IPv6 addresses or null) runs for every lane of every wave (lanes
 // without a record pass has == false) so that waves can cooperate inside it; it builds the key
@@ -162,15 +163,15 @@ struct rtn_ct_frames {  // this lane's frame in each of the wave's RTN_CT_GPW gr
 
 __device__ __forceinline__ void rtn_ct_load(const rtn_ct_args& a, rtn_ct_frames& f) {
   constexpr rtn_u32 G = RTN_CT_GPW;
-  __shared__ rtn_u32 v6cnt[8];
+  __shared__ rtn_u32 v6cnt[RTN_CT_GROUPS];
   const rtn_u32 lane = threadIdx.x & 63u;
   const rtn_u32 w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const rtn_u32 c = blockIdx.x;
   const rtn_u64 lane_lt = lane ? (~0ull >> (64u - lane)) : 0ull;
   const rtn_u32 nw = (a.n + 63u) / 64u;
   const rtn_u64 nch = ((rtn_u64)a.n + RTN_CT_CHUNK - 1u) / RTN_CT_CHUNK;
-  // the chunk's bitmap words: lane j < 8 holds word j; pre[j] = records before group j
-  const rtn_u32 gj = c * (RTN_CT_CHUNK / 64u) + (lane & 7u);
+  // the chunk's bitmap words: lane j < RTN_CT_GROUPS holds word j; pre[j] = records before group j
+  const rtn_u32 gj = c * RTN_CT_GROUPS + (lane & (RTN_CT_GROUPS - 1u));
   const rtn_u64 word = gj < nw ? a.fwd_bm[gj] : 0ull;
   const rtn_u32 pop = (rtn_u32)__popcll(word);
   // (q = w * G + u is not a compile-time index: accumulate per group instead of indexing an array)
@@ -178,7 +179,7 @@ __device__ __forceinline__ void rtn_ct_load(const rtn_ct_args& a, rtn_ct_frames&
 #pragma unroll
   for (rtn_u32 u = 0; u < G; ++u) pre[u] = 0u;
 #pragma unroll
-  for (rtn_u32 j = 0; j < 8u; ++j) {
+  for (rtn_u32 j = 0; j < RTN_CT_GROUPS; ++j) {
     const rtn_u32 pj = __shfl(pop, (int)j);
 #pragma unroll
     for (rtn_u32 u = 0; u < G; ++u) pre[u] += j < w * G + u ? pj : 0u;

@@ -31,10 +31,12 @@ typedef unsigned int rtn_v4u __attribute__((ext_vector_type(4)));
 #define RTN_DELIVER_WORDS 0
 #endif
 #define RTN_DM_WORDS (RTN_DELIVER_WORDS > 0 ? RTN_DELIVER_WORDS : 1)
-// groups per output chunk: 512 frames (RTN_CHUNK_FRAMES in retina_pc.h). A chunk is one wave's
-// unit of work; at 2^25 frames 8 groups measured 6-9 % faster than 16 (the last chunks finish
-// sooner) and 2-3 % faster than 4 (fewer partial record blocks).
-#define RTN_CHUNK_GROUPS 8u
+// groups per output chunk: 256 frames (RTN_CHUNK_FRAMES in retina_pc.h). A chunk is one wave's
+// unit of work. In-process A/B with the interleaved record blocks and non-temporal stores (round
+// 2, four boxes): 256-frame chunks cfg2 -3.1 to -3.6 % against 512 (128-frame chunks +4 %;
+// 512-frame chunks in 128-thread blocks, +1 %). (Round 1, before those two: 512 beat 1024 by 6-9 %
+// and 256 by 2-3 %.)
+#define RTN_CHUNK_GROUPS 4u
 // Record-block stores (records, rtn_conn_t, IPv6 addresses) are non-temporal: each line is
 // written once and read by a later launch, so it streams past the caches (measured against plain
 // stores, in-process on one box, with the interleaved record layout: cfg2 -1.1 %, cfg3 -14.5 %,
@@ -65,15 +67,15 @@ struct rtn_args {
                               // bit4: compact ext rows (RTN_BATCH_EXT_COMPACT)
   rtn_u64* pc_bm;             // [ceil(n/64)]  PacketContinue bit
   rtn_u64* fwd_bm;            // [ceil(n/64)]  PacketContinue && L4Context::new Ok
-  rtn_l4rec* recs;            // [ceil(n/512)*512], dense per chunk
+  rtn_l4rec* recs;            // [ceil(n/256)*256], dense per chunk
   unsigned char* addr6;       // [ceil(n/64)*64][32] (src, dst) raw bytes, IPv6 records only
   rtn_u64* dlv_bm;            // [ceil(n/64)]  any packet-level delivery
-  rtn_u64* dlv_recs;          // [ceil(n/512)*512][RTN_DELIVER_WORDS] statement masks, ranked by dlv_bm per chunk
+  rtn_u64* dlv_recs;          // [ceil(n/256)*256][RTN_DELIVER_WORDS] statement masks, ranked by dlv_bm per chunk
   rtn_u32* counters;          // [0] pc, [1] fwd, [2] dlv, [3] status, [4..5] bytes, [6..7] ignored bytes,
                               // [8] tcp, [9] udp (forwarded), [10..11] tcp bytes, [12..13] udp bytes
   const unsigned char* ext;   // split layout: bytes 64..127 of each frame (64-byte slots), or null
-  rtn_u64* conn;              // optional [ceil(n/512)*512] rtn_conn_t, indexed like recs (flags bit2)
-  rtn_u64* conn_dlv;          // [ceil(n/512)*512][RTN_CONN_WORDS] first-packet statement masks
+  rtn_u64* conn;              // optional [ceil(n/256)*256] rtn_conn_t, indexed like recs (flags bit2)
+  rtn_u64* conn_dlv;          // [ceil(n/256)*256][RTN_CONN_WORDS] first-packet statement masks
   const rtn_u32* ext_chunk;   // flags bit4 (compact ext): row of each chunk's first needing frame
   rtn_u32 ext_rows;           // ... and the rows ext holds
   rtn_u32 pad;
@@ -732,19 +734,19 @@ struct rtn_pd_args {
 // groups (64 frames) per wave (1, 2, 4 and 8 measured within 3 % on cfg2: 0.40-0.41 ms; 1 is
 // the fastest)
 #define RTN_PD_GPW 1u
-#define RTN_PD_THREADS (512u / RTN_PD_GPW)
+#define RTN_PD_THREADS (64u * RTN_CHUNK_GROUPS / RTN_PD_GPW)
 
-// One block per 512-frame chunk, RTN_PD_GPW 64-frame groups per wave, one lane per frame of each.
+// One block per chunk, RTN_PD_GPW 64-frame groups per wave, one lane per frame of each.
 extern "C" __global__ void __launch_bounds__(RTN_PD_THREADS) rtn_pd_kernel(rtn_pd_args a) {
   constexpr rtn_u32 G = RTN_PD_GPW;
-  __shared__ rtn_u32 v6n[8];
+  __shared__ rtn_u32 v6n[RTN_CHUNK_GROUPS];
   const rtn_u32 lane = threadIdx.x & 63u;
   const rtn_u32 w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const rtn_u32 ch = blockIdx.x;
   const rtn_u32 nw = (a.n + 63u) >> 6;
   const rtn_u64 lane_lt = lane ? (~0ull >> (64u - lane)) : 0ull;
-  // the chunk's bitmap words: lane j < 8 holds word j; pre[j] = records before group j
-  const rtn_u32 gj = ch * 8u + (lane & 7u);
+  // the chunk's bitmap words: lane j < RTN_CHUNK_GROUPS holds word j; pre[j] = records before group j
+  const rtn_u32 gj = ch * RTN_CHUNK_GROUPS + (lane & (RTN_CHUNK_GROUPS - 1u));
   const rtn_u64 wj = gj < nw ? a.fwd_bm[gj] : 0ull;
   const rtn_u32 pop = (rtn_u32)__popcll(wj);
   // (q = w * G + u is not a compile-time index: accumulate per group instead of indexing an array)
@@ -752,7 +754,7 @@ extern "C" __global__ void __launch_bounds__(RTN_PD_THREADS) rtn_pd_kernel(rtn_p
 #pragma unroll
   for (rtn_u32 u = 0; u < G; ++u) pre[u] = 0u;
 #pragma unroll
-  for (rtn_u32 j = 0; j < 8u; ++j) {
+  for (rtn_u32 j = 0; j < RTN_CHUNK_GROUPS; ++j) {
     const rtn_u32 pj = __shfl(pop, (int)j);
 #pragma unroll
     for (rtn_u32 u = 0; u < G; ++u) pre[u] += j < w * G + u ? pj : 0u;
@@ -764,7 +766,7 @@ extern "C" __global__ void __launch_bounds__(RTN_PD_THREADS) rtn_pd_kernel(rtn_p
   for (rtn_u32 u = 0; u < G; ++u) {
     const rtn_u32 q = w * G + u;
     const rtn_u64 word = __shfl(wj, (int)q);
-    has[u] = ch * 8u + q < nw && ((word >> lane) & 1ull);
+    has[u] = ch * RTN_CHUNK_GROUPS + q < nw && ((word >> lane) & 1ull);
     r[u] = rtn_rec_slot(rtn_nchunks(a.n), ch, pre[u] + (rtn_u32)__popcll(word & lane_lt));
 #pragma unroll
     for (int j = 0; j < 6; ++j) rec[u][j] = 0u;
@@ -819,8 +821,8 @@ extern "C" __global__ void __launch_bounds__(RTN_PD_THREADS) rtn_pd_kernel(rtn_p
     if (on[u] && (sv[u][0] & 1u)) {
       rtn_u32 p6 = 0u;
 #pragma unroll
-      for (rtn_u32 j = 0; j < 8u; ++j) p6 += j < q ? v6n[j] : 0u;
-      const rtn_u64 r6 = (rtn_u64)ch * 512u + p6 + (rtn_u32)__popcll(m6[u] & lane_lt);
+      for (rtn_u32 j = 0; j < RTN_CHUNK_GROUPS; ++j) p6 += j < q ? v6n[j] : 0u;
+      const rtn_u64 r6 = (rtn_u64)ch * (64u * RTN_CHUNK_GROUPS) + p6 + (rtn_u32)__popcll(m6[u] & lane_lt);
       rtn_cview c;
       c.v6 = v6;
       c.v4 = !v6;
@@ -844,7 +846,7 @@ extern "C" __global__ void __launch_bounds__(RTN_PD_THREADS) rtn_pd_kernel(rtn_p
         }
       }
       // Payload::from_mbuf (datatypes/src/packet.rs:18-29): get_data_slice(offset, length)
-      const rtn_u32 dlen = a.dlen[(ch * 8u + q) * 64u + lane];
+      const rtn_u32 dlen = a.dlen[(ch * RTN_CHUNK_GROUPS + q) * 64u + lane];
       const rtn_u32 off = ((rec[u][5] & 0x3fu) << 2) | 2u, len = rec[u][5] >> 16;
       const bool pok = off < dlen && off + len <= dlen;
       rtn_pd_filter(c, pok, &sv[u][1], cnt);
@@ -852,7 +854,7 @@ extern "C" __global__ void __launch_bounds__(RTN_PD_THREADS) rtn_pd_kernel(rtn_p
       for (int j = 0; j < RTN_PD_S; ++j) dl = dl || cnt[j] != 0u;
     }
     const rtn_u64 mb = __ballot(dl);
-    if (lane == 0u && ch * 8u + q < nw) a.pd_bm[ch * 8u + q] = mb;
+    if (lane == 0u && ch * RTN_CHUNK_GROUPS + q < nw) a.pd_bm[ch * RTN_CHUNK_GROUPS + q] = mb;
     if (dl) {
 #pragma unroll
       for (int j = 0; j < RTN_PD_S; ++j) {

@@ -785,9 +785,9 @@ int32_t rtn_ct_process(rtn_ct_t* ct, const rtn_pc_out_t* pc, uint32_t n, rtn_ct_
   const bool spread = false;
 #endif
   a.check = spread ? 0u : 1u;
-  const uint32_t chunks = (n + RTN_CHUNK_FRAMES - 1u) / RTN_CHUNK_FRAMES;  // one 512-thread block each
+  const uint32_t chunks = (n + RTN_CHUNK_FRAMES - 1u) / RTN_CHUNK_FRAMES;  // one block each
   void* p[] = {&a};
-  const uint32_t threads = 512u / groups_per_wave("RTN_CT_GPW", RTN_CT_GPW);  // a chunk per block
+  const uint32_t threads = RTN_CHUNK_FRAMES / groups_per_wave("RTN_CT_GPW", RTN_CT_GPW);  // a chunk per block
   hipError_t e = hipModuleLaunchKernel(ct->insert, chunks, 1, 1, threads, 1, 1, 0, s, p, nullptr);
   if (e != hipSuccess) return hip_fail("rtn_ct_insert", e);
   e = hipModuleLaunchKernel(ct->lookup, chunks, 1, 1, threads, 1, 1, 0, s, p, nullptr);

@@ -381,7 +381,7 @@ class PCOutputs:
         return out
 
 
-CHUNK_FRAMES = 512  # RTN_CHUNK_FRAMES (include/retina_pc.h)
+CHUNK_FRAMES = 256  # RTN_CHUNK_FRAMES (include/retina_pc.h)
 
 
 def _rank_index(frames: np.ndarray) -> np.ndarray:
@@ -476,7 +476,7 @@ class PacketContinue:
         then holds bytes [0, 64) of every frame (stride 64) and `ext` bytes [64, 128).
         dl_le64 asserts that every data_len is <= 64 (RTN_BATCH_DL_LE64), which 64-byte slots
         without ext need unless `out` has counters (include/retina_pc.h). `ext_chunk` (device
-        uint32, one per 512-frame chunk) selects the compact split layout: `ext` then holds rows
+        uint32, one per CHUNK_FRAMES-frame chunk) selects the compact split layout: `ext` then holds rows
         only for the frames rtn_ext_needed() names (split_slab(..., compact=True))."""
         import torch
 
@@ -741,7 +741,7 @@ class PcapReader:
     def next_batch_split(self, head: np.ndarray, ext: np.ndarray, ext_chunk: np.ndarray,
                          data_len: np.ndarray) -> tuple[int, int]:
         """The compact split layout (RTN_BATCH_EXT_COMPACT): head (uint8, cap*64), ext (uint8,
-        rows*64), ext_chunk (uint32, ceil(cap/512)), data_len (uint16[cap]) -> (frames, ext rows)."""
+        rows*64), ext_chunk (uint32, ceil(cap/CHUNK_FRAMES)), data_len (uint16[cap]) -> (frames, ext rows)."""
         cap = len(data_len)
         assert head.size >= cap * 64 and ext.size % 64 == 0 and ext_chunk.size >= (cap + CHUNK_FRAMES - 1) // CHUNK_FRAMES
         n, rows = C.c_uint32(), C.c_uint32()

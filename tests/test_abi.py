@@ -70,10 +70,12 @@ def test_hiprtc_builds_gfx950_code_object(fset):
 def test_output_sizes():
     L = pc.lib()
     assert L.rtn_out_bitmap_bytes(65) == 16
-    assert L.rtn_out_l4_bytes(65) == 512 * 24
-    assert L.rtn_out_l4_bytes(1025) == 1536 * 24
-    assert L.rtn_out_addr6_bytes(1) == 512 * 32
-    assert L.rtn_out_dlv_bytes(64, 2) == 512 * 2 * 8      # masks only: the frame is the rank in dlv_bitmap
+    CF = pc.CHUNK_FRAMES
+    assert CF == 256
+    assert L.rtn_out_l4_bytes(65) == CF * 24
+    assert L.rtn_out_l4_bytes(1025) == 1280 * 24
+    assert L.rtn_out_addr6_bytes(1) == CF * 32
+    assert L.rtn_out_dlv_bytes(64, 2) == CF * 2 * 8      # masks only: the frame is the rank in dlv_bitmap
     assert L.rtn_out_bitmap_bytes(0xFFFFFFFF) == ((1 << 32) // 64) * 8   # 64-bit arithmetic, no wrap
     assert L.rtn_out_l4_bytes(0xFFFFFFFF) == (1 << 32) * 24
 
@@ -105,15 +107,15 @@ def test_headers_are_c(tmp_path):
 
 def test_rec_index_macro_matches_host_decoder(tmp_path):
     """RTN_REC_INDEX (retina_pc.h) and pc._rec_index (the decoder the parity tests use) agree, and
-    the index is a bijection of every (chunk, rank) pair onto [0, ceil(n/512)*512)."""
+    the index is a bijection of every (chunk, rank) pair onto [0, ceil(n/CF)*CF)."""
     import subprocess
 
     import numpy as np
 
     inc = Path(__file__).resolve().parent.parent / "include"
     src = ('#include "retina_pc.h"\n#include <stdio.h>\n#include <inttypes.h>\n'
-           "int main(void) {\n  const uint32_t ns[] = {1u, 511u, 512u, 513u, 4097u, 33554432u};\n"
-           "  for (int i = 0; i < 6; ++i) for (uint32_t c = 0; c < 3; ++c) for (uint32_t k = 0; k < 512; k += 37)\n"
+           "int main(void) {\n  const uint32_t ns[] = {1u, 255u, 256u, 257u, 4097u, 33554432u};\n"
+           "  for (int i = 0; i < 6; ++i) for (uint32_t c = 0; c < 3; ++c) for (uint32_t k = 0; k < RTN_CHUNK_FRAMES; k += 37)\n"
            '    printf("%u %u %u %" PRIu64 "\\n", ns[i], c, k, RTN_REC_INDEX(ns[i], c, k));\n  return 0;\n}\n')
     (tmp_path / "ri.c").write_text(src)
     r = subprocess.run(["gcc", "-std=c11", "-Wall", "-Werror", f"-I{inc}", str(tmp_path / "ri.c"), "-o",
@@ -122,13 +124,14 @@ def test_rec_index_macro_matches_host_decoder(tmp_path):
     out = subprocess.run([str(tmp_path / "ri")], capture_output=True, text=True, check=True).stdout
     for line in out.splitlines():
         n, c, k, want = map(int, line.split())
-        frames = c * 512 + np.arange(k + 1)  # the chunk's first k+1 frames, all forwarded
+        frames = c * pc.CHUNK_FRAMES + np.arange(k + 1)  # the chunk's first k+1 frames, all forwarded
         assert pc._rec_index(frames, n)[-1] == want
     for n in (1, 700, 5000):
-        nch = (n + 511) // 512
-        frames = np.arange(nch * 512)  # every slot of every chunk forwarded
+        cf = pc.CHUNK_FRAMES
+        nch = (n + cf - 1) // cf
+        frames = np.arange(nch * cf)  # every slot of every chunk forwarded
         idx = pc._rec_index(frames, n)
-        assert np.array_equal(np.sort(idx), np.arange(nch * 512))
+        assert np.array_equal(np.sort(idx), np.arange(nch * cf))
 
 
 _RUST_C = {"u8": "uint8_t", "u16": "uint16_t", "u32": "uint32_t", "u64": "uint64_t", "i32": "int32_t",
@@ -244,7 +247,7 @@ def test_ext_needed_rule_matches_header(tmp_path):
     py_rule = pc.ext_needed(slab, dlen)
     assert np.array_equal(c_rule, py_rule) and 0 < py_rule.sum() < len(dlen)
     head, ext, chunk = pc.split_slab(slab.reshape(-1), 128, dlen, compact=True)
-    assert ext.size == 64 * int(py_rule.sum()) and chunk[0] == 0 and len(chunk) == (len(dlen) + 511) // 512
+    assert ext.size == 64 * int(py_rule.sum()) and chunk[0] == 0 and len(chunk) == (len(dlen) + pc.CHUNK_FRAMES - 1) // pc.CHUNK_FRAMES
     assert np.array_equal(ext.reshape(-1, 64), slab[py_rule, 64:128])
 
 

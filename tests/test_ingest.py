@@ -143,7 +143,7 @@ def test_split_batches_match_the_slot_layout(tmp_path, ext_cap):
     while True:
         head = np.zeros(cap * 64, np.uint8)
         ext = np.zeros((ext_cap or cap) * 64, np.uint8)
-        ch = np.zeros((cap + 511) // 512, np.uint32)
+        ch = np.zeros((cap + pc.CHUNK_FRAMES - 1) // pc.CHUNK_FRAMES, np.uint32)
         d = np.zeros(cap, np.uint16)
         k, rows = r.next_batch_split(head, ext, ch, d)
         if k == 0:
@@ -152,8 +152,8 @@ def test_split_batches_match_the_slot_layout(tmp_path, ext_cap):
         nd = pc.ext_needed(np.pad(hb, ((0, 0), (0, 64))), d[:k])
         assert rows == nd.sum() and (ext_cap is None or rows <= ext_cap)
         for c in range(len(ch)):
-            if c * 512 < k:
-                assert ch[c] == nd[:c * 512].sum()
+            if c * pc.CHUNK_FRAMES < k:
+                assert ch[c] == nd[:c * pc.CHUNK_FRAMES].sum()
         got_head.append(hb)
         got_dl.append(d[:k])
         got_ext.append(ext[:rows * 64].reshape(rows, 64))

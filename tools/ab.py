@@ -52,18 +52,17 @@ def main() -> None:
     if stride > 64:
         head, ext = pc.split_slab(slab, stride)
         lay["split"] = (torch.from_numpy(head).to(dev), 64, torch.from_numpy(ext).to(dev), None)
-        if args.compact or any(e.endswith(("#compact", "#compact256")) for e in args.entries):
+        if args.compact or any("#compact" in e for e in args.entries):
             h2, ext2, chunk = pc.split_slab(slab, stride, dlen, compact=True)
             lay["compact"] = (lay["split"][0], 64, torch.from_numpy(ext2).to(dev),
                               torch.from_numpy(chunk.view(np.int32)).to(dev))
-        if any(e.endswith("#compact256") for e in args.entries):
-            # the same ext rows, first rows per 256-frame chunk (timing of the chunk256 variant)
-            need = pc.ext_needed(slab.reshape(-1, stride), dlen).astype(np.int64)
-            per = np.add.reduceat(need, np.arange(0, n, 256))
-            c256 = np.concatenate([[0], np.cumsum(per)[:-1]]).astype(np.uint32)
-            h2, ext2, _ = pc.split_slab(slab, stride, dlen, compact=True)
-            lay["compact256"] = (lay["split"][0], 64, torch.from_numpy(ext2).to(dev),
-                                 torch.from_numpy(c256.view(np.int32)).to(dev))
+        for cf in (128, 256, 512):
+            if any(e.endswith(f"#compact{cf}") for e in args.entries):
+                # the same ext rows, first rows per cf-frame chunk (timing of the chunk-size variants)
+                need = pc.ext_needed(slab.reshape(-1, stride), dlen).astype(np.int64)
+                per = np.add.reduceat(need, np.arange(0, n, cf))
+                cx = np.concatenate([[0], np.cumsum(per)[:-1]]).astype(np.uint32)
+                lay[f"compact{cf}"] = (lay["split"][0], 64, lay["compact"][2], torch.from_numpy(cx.view(np.int32)).to(dev))
     if stride == 64 or args.mono or any(e.endswith("#mono") for e in args.entries):
         lay["mono"] = (torch.from_numpy(slab).to(dev), stride, None, None)
     default = "mono" if (stride == 64 or args.mono) else ("compact" if args.compact else "split")

@@ -130,16 +130,15 @@ VARIANTS.update({"oldform": oldform, "splitc_w4": splitc_w4, "splitc_pf": splitc
                  "st_ntsc1": _store_asm("nt sc1"), "st_nt": _store_asm("nt")})
 
 
-def chunk256(src: str) -> str:
-    """Timing only: 256-frame chunks (one wave per chunk, half the work unit; outputs are laid out
-    by 256-frame chunks, so only the plain split layout and 64-B slots apply). Run with @GRID =
-    ceil(n / 1024) blocks so that every chunk still gets its own wave."""
-    return _sub(src, "#define RTN_CHUNK_GROUPS 8u", "#define RTN_CHUNK_GROUPS 4u")
+def chunk512(src: str) -> str:
+    """Timing only: 512-frame chunks (the round-2 layout before 256; the compact layout needs
+    #compact512). Run with @GRID = ceil(n / 2048) blocks so that every chunk gets its own wave."""
+    return _sub(src, "#define RTN_CHUNK_GROUPS 4u", "#define RTN_CHUNK_GROUPS 8u")
 
 
 def chunk128(src: str) -> str:
     """Timing only: 128-frame chunks (@GRID = ceil(n / 512) blocks)."""
-    return _sub(src, "#define RTN_CHUNK_GROUPS 8u", "#define RTN_CHUNK_GROUPS 2u")
+    return _sub(src, "#define RTN_CHUNK_GROUPS 4u", "#define RTN_CHUNK_GROUPS 2u")
 
 
 def rb128(src: str) -> str:
@@ -155,7 +154,7 @@ def wpb2(src: str) -> str:
     return src
 
 
-VARIANTS.update({"chunk256": chunk256, "chunk128": chunk128, "rb128": rb128, "wpb2": wpb2})
+VARIANTS.update({"chunk512": chunk512, "chunk128": chunk128, "rb128": rb128, "wpb2": wpb2})
 
 
 def write(name: str, outdir: Path) -> Path:
