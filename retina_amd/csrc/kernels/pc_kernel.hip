@@ -78,7 +78,7 @@ struct rtn_args {
   rtn_u64* conn_dlv;          // [ceil(n/256)*256][RTN_CONN_WORDS] first-packet statement masks
   const rtn_u32* ext_chunk;   // flags bit4 (compact ext): row of each chunk's first needing frame
   rtn_u32 ext_rows;           // ... and the rows ext holds
-  rtn_u32 pad;
+  rtn_u32 cpw;                // compact split kernel: consecutive chunks per wave (1 or 2)
 };
 
 struct rtn_view {
@@ -590,7 +590,12 @@ __device__ __forceinline__ void rtn_run(const rtn_args& a) {
   rtn_v4u* ring6 = rtn_ring6[threadIdx.x >> 6];
   __shared__ __attribute__((aligned(16))) rtn_u32 rtn_tile[4][slots64 ? 64 * RTN_XPITCH : 1];
   rtn_u32* tile = rtn_tile[threadIdx.x >> 6];
-  for (rtn_u32 c = wave_g; c < nchunks; c += nwaves) {
+  // The compact split kernel may walk cpw consecutive chunks per wave (the runtime picks 2 when
+  // the kernel's registers allow fewer than 4 waves per SIMD: in-process A/B, cfg4 (3 waves)
+  // 0.1772 -> 0.1722 ms with 2, cfg3 (4 waves) 0.2656 -> 0.2754 ms, so 1 there).
+  const rtn_u32 cpw = MODE == RTN_SPLITC ? a.cpw : 1u;
+  for (rtn_u32 cw = wave_g * cpw; cw < nchunks; cw += nwaves * cpw)
+  for (rtn_u32 c = cw; c < cw + cpw && c < nchunks; ++c) {
     const rtn_u32 gb = c * RTN_CHUNK_GROUPS;
     const rtn_u32 ge = gb + RTN_CHUNK_GROUPS < nw ? gb + RTN_CHUNK_GROUPS : nw;
     rtn_chunk ch = {(rtn_u64)c * (64u * RTN_CHUNK_GROUPS), 0u, 0u, 0u, 0u, 0u, 0u, 0ull, 0ull, 0ull};

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
 
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
@@ -218,7 +219,7 @@ struct KArgs {
   uint64_t* conn_dlv;
   const uint32_t* ext_chunk;
   uint32_t ext_rows;
-  uint32_t pad;
+  uint32_t cpw;
 };
 
 // Groups per wave of a kernel (RTN_PD_GPW / RTN_CT_GPW): the default, unless an RTN_KERNEL_DEFINES
@@ -267,6 +268,7 @@ struct rtn_pc {
   hipFunction_t fn_pd = nullptr;     // rtn_pd_kernel: the PacketDeliver filter (rtn_pd_run)
   uint32_t blocks = 0;
   uint32_t threads = 256;  // threads per block of the packet kernel (4 waves, one chunk each)
+  uint32_t splitc_cpw = 1;  // chunks per wave of rtn_pc_kernel_splitc (rtn_args.cpw)
   // used when the caller passes no counters: word RTN_CNT_STATUS accumulates the status bits of
   // such runs until rtn_pc_take_status reads and clears them (the other words are never read)
   uint32_t* scratch_counters = nullptr;
@@ -475,6 +477,18 @@ int32_t rtn_pc_create_from_program(rtn_program_t* p, int device, rtn_pc_t** out)
   if (e != hipSuccess) return fail(RTN_EDEVICE, std::string("hipModuleGetFunction: ") + hipGetErrorString(e));
   e = hipModuleGetFunction(&pc->fn_splitc, pc->module, "rtn_pc_kernel_splitc");
   if (e != hipSuccess) return fail(RTN_EDEVICE, std::string("hipModuleGetFunction: ") + hipGetErrorString(e));
+  {
+    // two consecutive chunks per wave when the compact split kernel's VGPRs hold it below 4
+    // waves per SIMD (its LDS allows 4): see the chunk loop in pc_kernel.hip
+    int vgprs = 0;
+    if (hipFuncGetAttribute(&vgprs, HIP_FUNC_ATTRIBUTE_NUM_REGS, pc->fn_splitc) == hipSuccess && vgprs > 0) {
+      const int regs = (vgprs + 7) / 8 * 8;  // allocation granule
+      pc->splitc_cpw = 512 / regs < 4 ? 2u : 1u;
+    }
+#ifdef RTN_EXPERIMENTS
+    if (getenv("RTN_DEBUG")) fprintf(stderr, "rtn_pc_kernel_splitc: %d VGPRs, %u chunks per wave\n", vgprs, pc->splitc_cpw);
+#endif
+  }
   e = hipModuleGetFunction(&pc->fn_pd, pc->module, "rtn_pd_kernel");
   if (e != hipSuccess) return fail(RTN_EDEVICE, std::string("hipModuleGetFunction: ") + hipGetErrorString(e));
   e = hipMalloc(&pc->scratch_counters, RTN_COUNTERS_BYTES);
@@ -484,6 +498,7 @@ int32_t rtn_pc_create_from_program(rtn_program_t* p, int device, rtn_pc_t** out)
 #ifdef RTN_EXPERIMENTS
   if (const char* g = getenv("RTN_GRID")) pc->blocks = (uint32_t)strtoul(g, nullptr, 10);
   if (const char* b = getenv("RTN_BLOCK")) pc->threads = (uint32_t)strtoul(b, nullptr, 10);
+  if (const char* c = getenv("RTN_CPW")) pc->splitc_cpw = (uint32_t)strtoul(c, nullptr, 10);
 #endif
   *out = pc.release();
   return RTN_OK;
@@ -549,7 +564,7 @@ int32_t rtn_pc_run(rtn_pc_t* pc, const rtn_batch_t* in, rtn_pc_out_t* out, void*
             ((in->flags & RTN_BATCH_DL_LE64) ? 8u : 0u) | ((in->flags & RTN_BATCH_EXT_COMPACT) ? 16u : 0u);
   a.ext_chunk = in->ext_chunk;
   a.ext_rows = in->ext_rows;
-  a.pad = 0u;
+  a.cpw = (in->ext && (in->flags & RTN_BATCH_EXT_COMPACT)) ? pc->splitc_cpw : 1u;
   a.pc_bm = out->pc_bitmap;
   a.fwd_bm = out->fwd_bitmap;
   a.recs = out->l4;
@@ -564,7 +579,8 @@ int32_t rtn_pc_run(rtn_pc_t* pc, const rtn_batch_t* in, rtn_pc_out_t* out, void*
   // default: one wave per chunk (4 chunks per 256-thread block); the hardware dispatcher hands
   // out blocks as earlier ones retire, which balances the tail better than a persistent grid
   const uint32_t threads = pc->threads;
-  const uint32_t need = (chunks + threads / 64u - 1u) / (threads / 64u);
+  const uint32_t per_block = (threads / 64u) * a.cpw;  // chunks per block
+  const uint32_t need = (chunks + per_block - 1u) / per_block;
   uint32_t blocks = pc->blocks ? pc->blocks : need;
 #ifndef RTN_EXPERIMENTS
   if (blocks > need) blocks = need;

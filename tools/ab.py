@@ -1,6 +1,6 @@
 """In-process A/B timing of kernel variants on one GPU (tools/README.md).
 
-    python tools/ab.py cfg2|cfg3|cfg4 VARIANT[:DEFINES][@GRID][#split|#compact|#mono] ... [--reps R]
+    python tools/ab.py cfg2|cfg3|cfg4 VARIANT[:DEFINES][@GRID][^CPW][#split|#compact|#mono] ... [--reps R]
         [--frames N] [--mono] [--compact]
 
 VARIANT names a tools/variants.py function (or several joined with '+'). Prints, per entry, the
@@ -73,6 +73,11 @@ def main() -> None:
     ctxs, out = [], None
     for e in args.entries:
         name, _, layout = e.partition("#")
+        name, _, cpw = name.partition("^")  # VARIANT^N: N chunks per wave in the compact split kernel
+        if cpw:
+            os.environ["RTN_CPW"] = cpw
+        else:
+            os.environ.pop("RTN_CPW", None)
         name, _, grid = name.partition("@")
         name, _, defs = name.partition(":")
         os.environ["RTN_KERNEL_TEMPLATE"] = str(variants.write(name, tmp))

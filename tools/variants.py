@@ -154,7 +154,16 @@ def wpb2(src: str) -> str:
     return src
 
 
-VARIANTS.update({"chunk512": chunk512, "chunk128": chunk128, "rb128": rb128, "wpb2": wpb2})
+def cpw2(src: str) -> str:
+    """The compact split kernel walks two consecutive chunks per wave (a 512-frame work unit over
+    the 256-frame layout); @GRID = ceil(n / 2048)."""
+    return _sub(src, "  for (rtn_u32 c = wave_g; c < nchunks; c += nwaves) {",
+                "  constexpr rtn_u32 CPW = MODE == RTN_SPLITC ? 2u : 1u;\n"
+                "  for (rtn_u32 cw = wave_g * CPW; cw < nchunks; cw += nwaves * CPW)\n"
+                "  for (rtn_u32 c = cw; c < cw + CPW && c < nchunks; ++c) {")
+
+
+VARIANTS.update({"cpw2": cpw2, "chunk512": chunk512, "chunk128": chunk128, "rb128": rb128, "wpb2": wpb2})
 
 
 def write(name: str, outdir: Path) -> Path:
