@@ -400,6 +400,10 @@ def main() -> None:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--settle-ms", type=float, default=250.0,
+                    help="before the warmup steps, run the step back to back for this long (untimed): "
+                         "the first ~10 ms of launches on a fresh process run 5-15 %% slower "
+                         "(tools/warm_probe.py, DESIGN.md §4)")
     ap.add_argument("--config", default="cfg2", choices=list(CONFIGS))
     ap.add_argument("--frames", type=int, default=0, help="frames per GPU (default: the config's)")
     ap.add_argument("--no-cpu", action="store_true")
@@ -477,6 +481,14 @@ def main() -> None:
     out = ctx.alloc_outputs(n, addr6=True, counters=False)
     stream = torch.cuda.current_stream(dev)
 
+    # settle: the device's first ~10 ms of this load run slower (measured per 10-launch window from
+    # a process's first launch: cfg3 0.297 -> 0.265 ms, cfg4 0.202 -> 0.176 ms after ~50 launches);
+    # untimed, same step, outside the timed region
+    t_settle = time.perf_counter()
+    while (time.perf_counter() - t_settle) * 1e3 < args.settle_ms:
+        for _ in range(10):
+            ctx.run(d_slab, run_stride, d_dlen, n, out, stream=stream, ext=d_ext, dl_le64=dl_le64, ext_chunk=d_chunk)
+        torch.cuda.synchronize(dev)
     for _ in range(args.warmup):
         ctx.run(d_slab, run_stride, d_dlen, n, out, stream=stream, ext=d_ext, dl_le64=dl_le64, ext_chunk=d_chunk)
     torch.cuda.synchronize(dev)
@@ -575,6 +587,7 @@ def main() -> None:
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "settle_ms": args.settle_ms,
             "ms_per_step": round(wall / args.steps * 1e3, 4),
             "higher_is_better": True,
             "scaling": "weak",

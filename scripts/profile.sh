@@ -16,6 +16,6 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gp
 i=0
 for C in FETCH_SIZE WRITE_SIZE "TCC_EA0_RDREQ TCC_EA0_RDREQ_128B TCC_EA0_WRREQ TCC_EA0_WRREQ_64B" "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_VMEM SQ_INSTS_LDS"; do
   i=$((i+1))
-  timeout -s KILL 120 rocprofv3 --pmc $C --output-format csv -d "$R/gpurun_out/pmc_${TAG}_${CFG}_$i" -o run -- python bench.py --config $CFG --no-cpu --no-e2e --no-conn --steps 5 --warmup 1 > /dev/null 2> gpurun_out/pmc_${TAG}_${CFG}_$i.err || exit $?
+  timeout -s KILL 120 rocprofv3 --pmc $C --output-format csv -d "$R/gpurun_out/pmc_${TAG}_${CFG}_$i" -o run -- python bench.py --config $CFG --no-cpu --no-e2e --no-conn --steps 5 --warmup 1 --settle-ms 0 > /dev/null 2> gpurun_out/pmc_${TAG}_${CFG}_$i.err || exit $?
 done
 echo done
