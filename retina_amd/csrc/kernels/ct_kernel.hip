@@ -144,7 +144,12 @@ __device__ __forceinline__ rtn_u64* rtn_ct_tag(const rtn_ct_args& a, rtn_u32 slo
 #ifndef RTN_CT_GPW
 #define RTN_CT_GPW 2u  // 64-frame groups per wave (cfg2 steady pass: 1 -> 0.62, 2 -> 0.52, 4 -> 0.62, 8 -> 1.13 ms)
 #endif
-#define RTN_CT_BLOCK (64u * (RTN_CT_CHUNK / 64u) / RTN_CT_GPW)
+// Chunks per block. The insert pass's block takes 2 (4 waves), so its admission costs one
+// reservation atomic per 512 frames (one per 256-frame chunk: cfg2 first pass 1.37 -> 1.98 ms);
+// the lookup's takes 1 (2 waves: steady pass 0.512 ms with 2 chunks per block, 0.484 with 1).
+#define RTN_CT_INSERT_CPB 2u
+#define RTN_CT_LOOKUP_CPB 1u
+#define RTN_CT_WPC (RTN_CT_GROUPS / RTN_CT_GPW)  // waves per chunk
 
 // One block per chunk; each wave takes RTN_CT_GPW groups and issues all of their loads
 // before using any (the walk is latency-bound: a wave per group left too few loads in flight).
@@ -161,12 +166,15 @@ struct rtn_ct_frames {  // this lane's frame in each of the wave's RTN_CT_GPW gr
   const rtn_u32* a6[RTN_CT_GPW];
 };
 
+template <rtn_u32 CPB>
 __device__ __forceinline__ void rtn_ct_load(const rtn_ct_args& a, rtn_ct_frames& f) {
   constexpr rtn_u32 G = RTN_CT_GPW;
-  __shared__ rtn_u32 v6cnt[RTN_CT_GROUPS];
+  __shared__ rtn_u32 v6cnt_all[CPB][RTN_CT_GROUPS];
   const rtn_u32 lane = threadIdx.x & 63u;
-  const rtn_u32 w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const rtn_u32 c = blockIdx.x;
+  const rtn_u32 wb = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const rtn_u32 w = wb % RTN_CT_WPC;                   // wave within its chunk
+  const rtn_u32 c = blockIdx.x * CPB + wb / RTN_CT_WPC;
+  rtn_u32* v6cnt = v6cnt_all[wb / RTN_CT_WPC];
   const rtn_u64 lane_lt = lane ? (~0ull >> (64u - lane)) : 0ull;
   const rtn_u32 nw = (a.n + 63u) / 64u;
   const rtn_u64 nch = ((rtn_u64)a.n + RTN_CT_CHUNK - 1u) / RTN_CT_CHUNK;
@@ -229,12 +237,12 @@ __device__ __forceinline__ void rtn_ct_load_rec(const rtn_ct_args& a, rtn_ct_fra
   }
 }
 
-extern "C" __global__ void __launch_bounds__(RTN_CT_BLOCK) rtn_ct_insert(rtn_ct_args a) {
+extern "C" __global__ void __launch_bounds__(64u * RTN_CT_WPC * RTN_CT_INSERT_CPB) rtn_ct_insert(rtn_ct_args a) {
   constexpr rtn_u32 G = RTN_CT_GPW;
   __shared__ rtn_u32 blk[3];  // openers needing a new slot (then tickets drawn), reservation base, granted
   if (threadIdx.x == 0) blk[0] = 0u;
   rtn_ct_frames f;
-  rtn_ct_load(a, f);
+  rtn_ct_load<RTN_CT_INSERT_CPB>(a, f);
   const rtn_u32 lane = threadIdx.x & 63u;
   bool active[G];
   rtn_u32 slot[G];
@@ -370,10 +378,10 @@ __device__ __forceinline__ rtn_u32 rtn_ct_status(const rtn_ct_args& a, rtn_u32 e
   return frame > first ? RTN_CT_HIT : frame == first ? RTN_CT_NEW : (opens ? RTN_CT_NEW_DROPPED : RTN_CT_MISS);
 }
 
-extern "C" __global__ void __launch_bounds__(RTN_CT_BLOCK) rtn_ct_lookup(rtn_ct_args a) {
+extern "C" __global__ void __launch_bounds__(64u * RTN_CT_WPC * RTN_CT_LOOKUP_CPB) rtn_ct_lookup(rtn_ct_args a) {
   constexpr rtn_u32 G = RTN_CT_GPW;
   rtn_ct_frames f;
-  rtn_ct_load(a, f);
+  rtn_ct_load<RTN_CT_LOOKUP_CPB>(a, f);
   // Every group's first probe is issued before any is used: the start slot's occupancy bit (in
   // L2; most misses end here), then the tags of occupied start slots, then the slots whose tag
   // matches. Only chains (start slot held by another key or removed) probe further, one by one.

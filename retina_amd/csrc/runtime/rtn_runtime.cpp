@@ -684,6 +684,7 @@ struct rtn_ct {
 
 namespace {
 constexpr uint32_t RTN_CT_GPW = 2;  // must match ct_kernel.hip
+constexpr uint32_t RTN_CT_INSERT_CPB = 2, RTN_CT_LOOKUP_CPB = 1;  // chunks per block, must match ct_kernel.hip
 
 struct CtArgs {  // must match struct rtn_ct_args in ct_kernel.hip
   const uint64_t* fwd_bm;
@@ -801,12 +802,14 @@ int32_t rtn_ct_process(rtn_ct_t* ct, const rtn_pc_out_t* pc, uint32_t n, rtn_ct_
   const bool spread = false;
 #endif
   a.check = spread ? 0u : 1u;
-  const uint32_t chunks = (n + RTN_CHUNK_FRAMES - 1u) / RTN_CHUNK_FRAMES;  // one block each
+  const uint32_t chunks = (n + RTN_CHUNK_FRAMES - 1u) / RTN_CHUNK_FRAMES;
   void* p[] = {&a};
-  const uint32_t threads = RTN_CHUNK_FRAMES / groups_per_wave("RTN_CT_GPW", RTN_CT_GPW);  // a chunk per block
-  hipError_t e = hipModuleLaunchKernel(ct->insert, chunks, 1, 1, threads, 1, 1, 0, s, p, nullptr);
+  const uint32_t per_chunk = RTN_CHUNK_FRAMES / groups_per_wave("RTN_CT_GPW", RTN_CT_GPW);  // threads
+  const uint32_t iblocks = (chunks + RTN_CT_INSERT_CPB - 1u) / RTN_CT_INSERT_CPB;
+  hipError_t e = hipModuleLaunchKernel(ct->insert, iblocks, 1, 1, per_chunk * RTN_CT_INSERT_CPB, 1, 1, 0, s, p, nullptr);
   if (e != hipSuccess) return hip_fail("rtn_ct_insert", e);
-  e = hipModuleLaunchKernel(ct->lookup, chunks, 1, 1, threads, 1, 1, 0, s, p, nullptr);
+  const uint32_t lblocks = (chunks + RTN_CT_LOOKUP_CPB - 1u) / RTN_CT_LOOKUP_CPB;
+  e = hipModuleLaunchKernel(ct->lookup, lblocks, 1, 1, per_chunk * RTN_CT_LOOKUP_CPB, 1, 1, 0, s, p, nullptr);
   if (e != hipSuccess) return hip_fail("rtn_ct_lookup", e);
   return RTN_OK;
 }
