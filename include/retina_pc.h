@@ -258,6 +258,17 @@ int32_t rtn_pc_run(rtn_pc_t* pc, const rtn_batch_t* in, rtn_pc_out_t* out, void*
 /* RTN_STATUS_* bits raised by runs without counters since the last call, then cleared.
  * Synchronizes the device. */
 int32_t rtn_pc_take_status(rtn_pc_t* pc, uint32_t* status);
+/* accepted_idx / n_accepted (the compaction form of SURVEY §8(b)) from any of the output
+ * bitmaps (pc_bitmap, fwd_bitmap, dlv_bitmap), on `stream` after the run that wrote it:
+ * idx[k] = the frame index of the k-th set bit among frames [0, n), in frame order (idx holds
+ * up to n entries); *n_set = their count (both device memory). chunk_base (optional,
+ * [ceil(n / RTN_CHUNK_FRAMES) + 1]): the number of set bits before each chunk, so the record at
+ * RTN_REC_INDEX(n, c, k) belongs to frame idx[chunk_base[c] + k] (fwd_bitmap: l4, conn,
+ * rtn_ct_entry_t; dlv_bitmap: the record at dlv_records[c * RTN_CHUNK_FRAMES + k]), and
+ * chunk_base[last] = *n_set.
+ * Asynchronous; one scratch buffer per context, so calls on one context must not overlap. */
+int32_t rtn_pc_index(rtn_pc_t* pc, const uint64_t* bitmap, uint32_t n, uint32_t* idx, uint32_t* n_set,
+                     uint32_t* chunk_base, void* stream);
 /* Workgroups per launch (0 = default). */
 int32_t rtn_pc_set_grid(rtn_pc_t* pc, uint32_t blocks);
 int32_t rtn_pc_destroy(rtn_pc_t* pc);

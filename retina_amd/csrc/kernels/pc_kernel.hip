@@ -870,3 +870,107 @@ extern "C" __global__ void __launch_bounds__(RTN_PD_THREADS) rtn_pd_kernel(rtn_p
     }
   }
 }
+
+// ---------------------------------------------------------------------------------------------
+// accepted_idx / n_accepted (rtn_pc_index): the frame indices of a bitmap's set bits
+// in frame order, their count, and each chunk's first position in that order. Three launches: a
+// per-block popcount over RTN_IDX_WORDS bitmap words, an exclusive scan of the block sums in one
+// block, then per block a wave-level scan that writes the indices (lane = frame bit, one coalesced
+// store per word) and the chunk bases.
+#define RTN_IDX_WORDS 4096u  // bitmap words per block (4 waves x 1024)
+
+struct rtn_idx_args {
+  const rtn_u64* bm;
+  rtn_u32 n;          // frames
+  rtn_u32 nblocks;    // ceil(words / RTN_IDX_WORDS)
+  rtn_u32* block_sum; // [nblocks]: set bits per block, then their exclusive prefix
+  rtn_u32* idx;       // [set bits]
+  rtn_u32* n_set;     // [1]
+  rtn_u32* chunk_base;  // optional [nchunks + 1]
+};
+
+__device__ __forceinline__ rtn_u64 rtn_idx_word(const rtn_idx_args& a, rtn_u32 w) {
+  const rtn_u32 nw = (a.n + 63u) >> 6;
+  if (w >= nw) return 0ull;
+  const rtn_u64 x = a.bm[w];
+  const rtn_u32 tail = a.n & 63u;  // bits past n are not frames
+  return (w == nw - 1u && tail) ? x & ((1ull << tail) - 1ull) : x;
+}
+
+extern "C" __global__ void __launch_bounds__(256) rtn_idx_count(rtn_idx_args a) {
+  __shared__ rtn_u32 part[4];
+  const rtn_u32 w0 = blockIdx.x * RTN_IDX_WORDS;
+  rtn_u32 s = 0;
+  for (rtn_u32 j = threadIdx.x; j < RTN_IDX_WORDS; j += 256u) s += (rtn_u32)__popcll(rtn_idx_word(a, w0 + j));
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+  if ((threadIdx.x & 63u) == 0u) part[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0u) a.block_sum[blockIdx.x] = part[0] + part[1] + part[2] + part[3];
+}
+
+// one block of 1024 threads: exclusive prefix of the block sums in place, total to n_set
+extern "C" __global__ void __launch_bounds__(1024) rtn_idx_scan(rtn_idx_args a) {
+  __shared__ rtn_u32 wsum[16];
+  const rtn_u32 t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+  const rtn_u32 per = (a.nblocks + 1023u) / 1024u;  // consecutive block sums per thread
+  rtn_u32 local = 0;
+  for (rtn_u32 j = 0; j < per; ++j) {
+    const rtn_u32 b = t * per + j;
+    local += b < a.nblocks ? a.block_sum[b] : 0u;
+  }
+  rtn_u32 incl = local;  // inclusive scan within the wave
+  for (rtn_u32 off = 1; off < 64u; off <<= 1) {
+    const rtn_u32 y = __shfl_up(incl, off);
+    incl += lane >= off ? y : 0u;
+  }
+  if (lane == 63u) wsum[wv] = incl;
+  __syncthreads();
+  rtn_u32 before = 0;
+  for (rtn_u32 k = 0; k < wv; ++k) before += wsum[k];
+  rtn_u32 run = before + incl - local;  // exclusive prefix of this thread's first block
+  for (rtn_u32 j = 0; j < per; ++j) {
+    const rtn_u32 b = t * per + j;
+    if (b < a.nblocks) {
+      const rtn_u32 v = a.block_sum[b];
+      a.block_sum[b] = run;
+      run += v;
+    }
+  }
+  if (t == 1023u) {
+    a.n_set[0] = run;
+    if (a.chunk_base) a.chunk_base[(a.n + RTN_CHUNK_GROUPS * 64u - 1u) / (RTN_CHUNK_GROUPS * 64u)] = run;
+  }
+}
+
+extern "C" __global__ void __launch_bounds__(256) rtn_idx_write(rtn_idx_args a) {
+  __shared__ rtn_u32 wtot[4];
+  const rtn_u32 lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  const rtn_u64 lane_lt = lane ? (~0ull >> (64u - lane)) : 0ull;
+  const rtn_u32 wbeg = blockIdx.x * RTN_IDX_WORDS + wv * (RTN_IDX_WORDS / 4u);  // this wave's 1024 words
+  // this wave's total, then the waves before it
+  rtn_u32 s = 0;
+  for (rtn_u32 j = lane; j < RTN_IDX_WORDS / 4u; j += 64u) s += (rtn_u32)__popcll(rtn_idx_word(a, wbeg + j));
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+  if (lane == 0u) wtot[wv] = s;
+  __syncthreads();
+  rtn_u32 base = a.block_sum[blockIdx.x];
+  for (rtn_u32 k = 0; k < wv; ++k) base += wtot[k];
+  const rtn_u32 nw = (a.n + 63u) >> 6;
+  for (rtn_u32 j0 = 0; j0 < RTN_IDX_WORDS / 4u && wbeg + j0 < nw; j0 += 64u) {
+    const rtn_u64 mine = rtn_idx_word(a, wbeg + j0 + lane);  // lane l holds word j0 + l
+    const rtn_u32 c = (rtn_u32)__popcll(mine);
+    rtn_u32 incl = c;
+    for (rtn_u32 off = 1; off < 64u; off <<= 1) {
+      const rtn_u32 y = __shfl_up(incl, off);
+      incl += lane >= off ? y : 0u;
+    }
+    const rtn_u32 wd = wbeg + j0 + lane;
+    if (a.chunk_base && wd < nw && (wd % RTN_CHUNK_GROUPS) == 0u) a.chunk_base[wd / RTN_CHUNK_GROUPS] = base + incl - c;
+    for (rtn_u32 l = 0; l < 64u && wbeg + j0 + l < nw; ++l) {
+      const rtn_u64 word = __shfl(mine, (int)l);
+      const rtn_u32 wb = base + __shfl(incl - c, (int)l);
+      if ((word >> lane) & 1ull) a.idx[wb + (rtn_u32)__popcll(word & lane_lt)] = (wbeg + j0 + l) * 64u + lane;
+    }
+    base += __shfl(incl, 63);
+  }
+}

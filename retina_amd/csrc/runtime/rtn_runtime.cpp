@@ -248,6 +248,18 @@ struct PdArgs {
   uint64_t* pd_bm;
 };
 
+// must match struct rtn_idx_args in pc_kernel.hip
+struct IdxArgs {
+  const uint64_t* bm;
+  uint32_t n;
+  uint32_t nblocks;
+  uint32_t* block_sum;
+  uint32_t* idx;
+  uint32_t* n_set;
+  uint32_t* chunk_base;
+};
+constexpr uint32_t RTN_IDX_WORDS = 4096;  // bitmap words per block, must match pc_kernel.hip
+
 }  // namespace
 
 struct rtn_program {
@@ -266,6 +278,8 @@ struct rtn_pc {
   hipFunction_t fn_split = nullptr;  // rtn_pc_kernel_split: 64-byte slots + ext
   hipFunction_t fn_splitc = nullptr; // rtn_pc_kernel_splitc: 64-byte slots + compact ext rows
   hipFunction_t fn_pd = nullptr;     // rtn_pd_kernel: the PacketDeliver filter (rtn_pd_run)
+  hipFunction_t fn_idx[3] = {};      // rtn_idx_count / rtn_idx_scan / rtn_idx_write (rtn_pc_index)
+  uint32_t* idx_block_sum = nullptr; // their per-block sums (RTN_MAX_FRAMES / 64 / RTN_IDX_WORDS)
   uint32_t blocks = 0;
   uint32_t threads = 256;  // threads per block of the packet kernel (4 waves, one chunk each)
   uint32_t splitc_cpw = 1;  // chunks per wave of rtn_pc_kernel_splitc (rtn_args.cpw)
@@ -274,6 +288,7 @@ struct rtn_pc {
   uint32_t* scratch_counters = nullptr;
   ~rtn_pc() {
     if (scratch_counters) (void)hipFree(scratch_counters);
+    if (idx_block_sum) (void)hipFree(idx_block_sum);
     if (module) (void)hipModuleUnload(module);
     delete owned;
   }
@@ -491,6 +506,15 @@ int32_t rtn_pc_create_from_program(rtn_program_t* p, int device, rtn_pc_t** out)
   }
   e = hipModuleGetFunction(&pc->fn_pd, pc->module, "rtn_pd_kernel");
   if (e != hipSuccess) return fail(RTN_EDEVICE, std::string("hipModuleGetFunction: ") + hipGetErrorString(e));
+  {
+    const char* names[3] = {"rtn_idx_count", "rtn_idx_scan", "rtn_idx_write"};
+    for (int k = 0; k < 3; ++k) {
+      e = hipModuleGetFunction(&pc->fn_idx[k], pc->module, names[k]);
+      if (e != hipSuccess) return fail(RTN_EDEVICE, std::string("hipModuleGetFunction: ") + hipGetErrorString(e));
+    }
+  }
+  e = hipMalloc(&pc->idx_block_sum, (RTN_MAX_FRAMES / 64u / RTN_IDX_WORDS) * sizeof(uint32_t));
+  if (e != hipSuccess) return fail(RTN_EDEVICE, std::string("hipMalloc: ") + hipGetErrorString(e));
   e = hipMalloc(&pc->scratch_counters, RTN_COUNTERS_BYTES);
   if (e != hipSuccess) return fail(RTN_EDEVICE, std::string("hipMalloc: ") + hipGetErrorString(e));
   e = hipMemset(pc->scratch_counters, 0, RTN_COUNTERS_BYTES);
@@ -626,6 +650,32 @@ int32_t rtn_pd_run(rtn_pc_t* pc, const rtn_pc_out_t* out, const rtn_ct_entry_t* 
   hipError_t e = hipModuleLaunchKernel(pc->fn_pd, chunks, 1, 1, threads, 1, 1, 0, s, params, nullptr);
   if (e != hipSuccess) return fail(RTN_EDEVICE, std::string("hipModuleLaunchKernel: ") + hipGetErrorString(e));
   return RTN_OK;
+}
+
+int32_t rtn_pc_index(rtn_pc_t* pc, const uint64_t* bitmap, uint32_t n, uint32_t* idx, uint32_t* n_set,
+                     uint32_t* chunk_base, void* stream) {
+  if (!pc || !n_set || (n && (!bitmap || !idx))) return fail(RTN_EINVAL, "null argument");
+  if (n > RTN_MAX_FRAMES) return fail(RTN_EINVAL, "batch larger than RTN_MAX_FRAMES");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  hipError_t e = hipSetDevice(pc->device);
+  if (e == hipSuccess && n == 0) {
+    e = hipMemsetAsync(n_set, 0, 4, s);
+    if (e == hipSuccess && chunk_base) e = hipMemsetAsync(chunk_base, 0, 4, s);
+    return e == hipSuccess ? RTN_OK : fail(RTN_EDEVICE, std::string("hipMemsetAsync: ") + hipGetErrorString(e));
+  }
+  IdxArgs a;
+  a.bm = bitmap;
+  a.n = n;
+  a.nblocks = (uint32_t)((((uint64_t)n + 63u) / 64u + RTN_IDX_WORDS - 1u) / RTN_IDX_WORDS);
+  a.block_sum = pc->idx_block_sum;
+  a.idx = idx;
+  a.n_set = n_set;
+  a.chunk_base = chunk_base;
+  void* params[] = {&a};
+  const uint32_t grid[3] = {a.nblocks, 1u, a.nblocks}, threads[3] = {256u, 1024u, 256u};
+  for (int k = 0; k < 3 && e == hipSuccess; ++k)
+    e = hipModuleLaunchKernel(pc->fn_idx[k], grid[k], 1, 1, threads[k], 1, 1, 0, s, params, nullptr);
+  return e == hipSuccess ? RTN_OK : fail(RTN_EDEVICE, std::string("rtn_pc_index: ") + hipGetErrorString(e));
 }
 
 int32_t rtn_pc_take_status(rtn_pc_t* pc, uint32_t* status) {

@@ -96,6 +96,7 @@ EXPORTS = {
     "rtn_pc_run": (C.c_int32, [C.c_void_p, C.POINTER(_Batch), C.POINTER(_Out), C.c_void_p]),
     "rtn_pc_set_grid": (C.c_int32, [C.c_void_p, C.c_uint32]),
     "rtn_pc_take_status": (C.c_int32, [C.c_void_p, C.POINTER(C.c_uint32)]),
+    "rtn_pc_index": (C.c_int32, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "rtn_pc_destroy": (C.c_int32, [C.c_void_p]),
     "rtn_out_bitmap_bytes": (C.c_size_t, [C.c_uint32]),
     "rtn_out_l4_bytes": (C.c_size_t, [C.c_uint32]),
@@ -447,6 +448,23 @@ class PacketContinue:
         st = C.c_uint32()
         _check(lib().rtn_pc_take_status(self._h, C.byref(st)))
         return int(st.value)
+
+    def index(self, bitmap, n: int, chunk_base: bool = True, stream=None):
+        """rtn_pc_index: (idx, chunk_base) device tensors for a device bitmap of n frames: idx = the
+        frame indices of the set bits in frame order (accepted_idx), chunk_base = set bits before
+        each chunk (+ the total). Synchronizes to read n_set."""
+        import torch
+
+        dev = bitmap.device
+        idx = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+        n_set = torch.zeros(1, dtype=torch.int32, device=dev)
+        cb = torch.empty((n + CHUNK_FRAMES - 1) // CHUNK_FRAMES + 1, dtype=torch.int32, device=dev) if chunk_base else None
+        s = stream.cuda_stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
+        _check(lib().rtn_pc_index(self._h, C.c_void_p(bitmap.data_ptr()), n, C.c_void_p(idx.data_ptr()),
+                                  C.c_void_p(n_set.data_ptr()), C.c_void_p(cb.data_ptr() if cb is not None else 0),
+                                  C.c_void_p(s)))
+        k = int(n_set.item())
+        return idx[:k], cb
 
     def alloc_outputs(self, n: int, addr6: bool = True, counters: bool = True, conn: bool = False) -> PCOutputs:
         import torch
