@@ -123,7 +123,9 @@ uint64_t type_max(FT t) {
 
 bool is_int(FT t) { return t == FT::U8 || t == FT::U16 || t == FT::U32; }
 
-std::string u32lit(uint64_t v) { return std::to_string(v) + "u"; }
+// HIP literal of a predicate constant, wrapped in RTN_K (pc_kernel.hip: the identity unless a
+// timing variant redefines it)
+std::string u32lit(uint64_t v) { return "RTN_K(" + std::to_string(v) + "u)"; }
 
 struct Gen {
   PacketProgram& prog;
@@ -632,7 +634,7 @@ PacketProgram compile_packet_program(const std::vector<SubscriptionSpec>& subs) 
     g.rust += "  }\n";
   }
   prog.hip_body_branchy = "__device__ __forceinline__ void rtn_filter(const rtn_view& v, rtn_u32& act, rtn_u64* dm) {\n"
-                          "  (void)v; (void)dm;\n" +
+                          "  (void)v; (void)dm; RTN_KZ_DECL(v)\n" +
                           g.hip + "}\n";
   g.hip.clear();
   {
@@ -642,7 +644,7 @@ PacketProgram compile_packet_program(const std::vector<SubscriptionSpec>& subs) 
     if (g.flat_pc_stmt != prog.delivers.size()) throw FilterError("internal: packet-continue statement count");
   }
   prog.hip_body = "__device__ __forceinline__ void rtn_filter(const rtn_view& v, rtn_u32& act, rtn_u64* dm) {\n"
-                  "  (void)v; (void)dm;\n" +
+                  "  (void)v; (void)dm; RTN_KZ_DECL(v)\n" +
                   g.hip + "}\n";
   // The straight-line form evaluates every node for every frame; the nested form skips subtrees
   // no lane of a wave enters. Past kFlatMaxNodes the second wins (large disjoint subtrees).
@@ -666,7 +668,7 @@ PacketProgram compile_packet_program(const std::vector<SubscriptionSpec>& subs) 
   }
   prog.hip_conn_body =
       "__device__ __forceinline__ void rtn_conn_filter(const rtn_cview& c, rtn_u32& data, rtn_u32& term, rtn_u64* cm) "
-      "{\n  (void)c; (void)cm;\n" + gc.hip + "}\n";
+      "{\n  (void)c; (void)cm; RTN_KZ_DECL(c)\n" + gc.hip + "}\n";
   prog.rust_conn_listing = "let mut result = Actions::new();\n" +
                            std::string(c_any_pkt ? "if let Ok(ethernet) = parse_to::<Ethernet>(mbuf) {\n" : "") + gc.rust +
                            (c_any_pkt ? "}\n" : "") + "result\n";
@@ -686,7 +688,7 @@ PacketProgram compile_packet_program(const std::vector<SubscriptionSpec>& subs) 
   const bool d_wrap = !gd.rust.empty() && d_any_pkt;
   prog.hip_pd_body =
       "__device__ __forceinline__ void rtn_pd_filter(const rtn_cview& c, bool pok, const rtn_u32* f, rtn_u32* cnt) "
-      "{\n  (void)c; (void)pok; (void)f; (void)cnt;\n" + gd.hip + "}\n";
+      "{\n  (void)c; (void)pok; (void)f; (void)cnt; RTN_KZ_DECL(c)\n" + gd.hip + "}\n";
   prog.rust_pd_listing = std::string(d_wrap ? "if let Ok(ethernet) = parse_to::<Ethernet>(mbuf) {\n" : "") + gd.rust +
                          (d_wrap ? "}\n" : "");
   return prog;

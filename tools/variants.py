@@ -163,7 +163,26 @@ def cpw2(src: str) -> str:
                 "  for (rtn_u32 c = cw; c < cw + CPW && c < nchunks; ++c) {")
 
 
-VARIANTS.update({"cpw2": cpw2, "chunk512": chunk512, "chunk128": chunk128, "rb128": rb128, "wpb2": wpb2})
+def kz(src: str) -> str:
+    """Predicate constants XORed with a per-group run-time zero (readfirstlane(nrec >> 31)) so that
+    the compiler cannot hoist them out of the group loop into SGPRs (cfg4: 72 SGPR spills)."""
+    src = _sub(src, "#ifndef RTN_K\n", "#define RTN_K(c) ((c) ^ rtn_kz)\n#define RTN_KZ_DECL(x) const rtn_u32 rtn_kz = (x).kz;\n#ifndef RTN_K\n")
+    src = _sub(src, "struct rtn_view {\n", "struct rtn_view {\n  rtn_u32 kz;\n")
+    src = _sub(src, "struct rtn_cview {\n", "struct rtn_cview {\n  rtn_u32 kz;\n")
+    src = _sub(src, "  rtn_parse<NW>(w, dl, v);\n", "  rtn_parse<NW>(w, dl, v);\n  v.kz = __builtin_amdgcn_readfirstlane(ch.nrec >> 31);\n")
+    src = _sub(src, "      c.v6 = v.v6;\n", "      c.v6 = v.v6;\n      c.kz = v.kz;\n")
+    src = _sub(src, "      c.v6 = v6;\n", "      c.v6 = v6;\n      c.kz = 0u;\n")
+    return src
+
+
+def kzdm(src: str) -> str:
+    """kz, and the statement-mask bits (1 << b) XORed with the same zero."""
+    src = kz(src)
+    return _sub(src, "#define RTN_DM_SET(m, w, b, r) ((m)[w] |= (r) ? (1ull << (b)) : 0ull)",
+                "#define RTN_DM_SET(m, w, b, r) ((m)[w] |= (r) ? ((1ull << (b)) ^ (rtn_u64)rtn_kz) : 0ull)")
+
+
+VARIANTS.update({"kz": kz, "kzdm": kzdm, "cpw2": cpw2, "chunk512": chunk512, "chunk128": chunk128, "rb128": rb128, "wpb2": wpb2})
 
 
 def write(name: str, outdir: Path) -> Path:
