@@ -131,6 +131,7 @@ struct Gen {
   PacketProgram& prog;
   std::string hip, rust;
   FilterLayer layer = FilterLayer::PacketContinue;
+  bool range_runs = true;  // pc_flat lowers range runs (RangeRun)
 
   [[noreturn]] void type_error(const Predicate& p, const std::string& why) {
     throw FilterError("filter does not type-check (" + p.str() + "): " + why);
@@ -334,11 +335,108 @@ struct Gen {
       hip += "  RTN_DM_SET(dm, " + std::to_string(k / 64) + ", " + std::to_string(k % 64) + ", " + reach + ");\n";
     }
   }
+  // A run of sibling leaves that test one header field for equality against constants in
+  // arithmetic progression (`ipv4.dst_addr = 10.k.0.0/16` for k = 0..18; ports 80, 81, 82, ...),
+  // each delivering one packet-level statement with consecutive statement numbers and the same
+  // actions. The tests are mutually exclusive, so the run is one subtract-and-compare: the lane's
+  // offset into the progression picks its statement bit. The reach flags, the chain flag T and the
+  // statement bits come out as the per-child chain would produce them (pc_flat below).
+  struct RangeRun {
+    size_t len = 0;      // children in the run (0: no run here)
+    std::string x;       // the field (masked) as a u32 expression
+    uint64_t c0 = 0;     // its value at the run's first child
+    unsigned shift = 0;  // log2 of the progression's step
+  };
+  static constexpr size_t kRangeRunMin = 4;
+  bool range_key(const Predicate& p, std::string& x, uint64_t& c, unsigned& shift) const {
+    if (!p.is_binary() || !p.on_packet() || p.op != BinOp::Eq) return false;
+    const auto& tab = fields(p.protocol);
+    auto it = tab.find(p.field);
+    if (it == tab.end()) return false;
+    const FieldDef& fd = it->second;
+    if (p.value.kind == VKind::Int && is_int(fd.type) && p.value.i <= type_max(fd.type)) {
+      x = fd.hip, c = p.value.i, shift = 0;
+      return true;
+    }
+    if (p.value.kind == VKind::Ipv4 && fd.type == FT::V4 && p.value.v4.prefix >= 1) {
+      uint32_t mask = p.value.v4.netmask();
+      x = p.value.v4.prefix == 32 ? std::string(fd.hip) : "(" + std::string(fd.hip) + " & " + u32lit(mask) + ")";
+      c = p.value.v4.addr & mask, shift = 32 - p.value.v4.prefix;
+      return true;
+    }
+    return false;
+  }
+  RangeRun range_run(const PNode& n, size_t i, size_t stmt0) const {
+    RangeRun run;
+    const auto& ch = n.children;
+    auto leaf_one_stmt = [&](const PNode& c) {
+      for (auto& g : c.children)
+        if (g.pred.on_packet()) return false;
+      return c.deliver.size() == 1 && c.stream.empty();
+    };
+    std::string x0;
+    uint64_t c0;
+    unsigned s0;
+    if (!range_key(ch[i].pred, x0, c0, s0) || !leaf_one_stmt(ch[i])) return run;
+    const bool payload = stmt0 < prog.delivers.size() && prog.delivers[stmt0].payload;
+    size_t len = 1;
+    for (size_t j = i + 1; j < ch.size(); ++j, ++len) {
+      const PNode& c = ch[j];
+      std::string x;
+      uint64_t cv;
+      unsigned s;
+      if (!c.if_else || !range_key(c.pred, x, cv, s) || x != x0 || s != s0) break;
+      if (cv != c0 + (uint64_t(len) << s0) || !leaf_one_stmt(c) || !(c.actions == ch[i].actions)) break;
+      const size_t k = stmt0 + len;
+      if (k >= prog.delivers.size() || prog.delivers[k].payload != payload || (stmt0 % 64) + len >= 64) break;
+      if (prog.delivers[k].sub_id != (uint32_t)c.deliver.begin()->id) break;
+    }
+    if (len < kRangeRunMin) return run;
+    run.len = len, run.x = x0, run.c0 = c0, run.shift = s0;
+    return run;
+  }
+  void pc_flat_range(const PNode& n, size_t i, const RangeRun& run, const std::string& R, std::string& T,
+                     bool is_else) {
+    const PNode& first = n.children[i];
+    const std::string id = std::to_string(first.id);
+    const uint32_t k0 = flat_pc_stmt;
+    for (size_t j = 0; j < run.len; ++j) {
+      const uint32_t k = flat_pc_stmt++;
+      if (k >= prog.delivers.size() || prog.delivers[k].sub_id != (uint32_t)n.children[i + j].deliver.begin()->id)
+        throw FilterError("internal: packet-continue statement order");
+    }
+    const uint64_t span = uint64_t(run.len) << run.shift;  // <= 2^32: the keys are distinct u32 values
+    hip += "  const rtn_u32 q" + id + " = " + run.x + " - " + u32lit(run.c0) + ";\n";
+    hip += "  const bool k" + id + " = (unsigned long long)q" + id + " < " + std::to_string(span) + "ull;\n";
+    const std::string rc = "r" + id;
+    if (!is_else || T.empty()) {
+      T = "t" + id;
+      hip += "  bool " + T + " = k" + id + ";\n";
+      hip += "  const bool " + rc + " = " + R + " && k" + id + ";\n";
+    } else {
+      hip += "  const bool " + rc + " = " + R + " && !" + T + " && k" + id + ";\n";
+      hip += "  " + T + " = " + T + " || k" + id + ";\n";
+    }
+    if (!first.actions.drop()) hip += "  act |= " + rc + " ? " + u32lit(first.actions.data) + " : 0u;\n";
+    const std::string reach = prog.delivers[k0].payload ? "(" + rc + " && v.payload_ok)" : rc;
+    hip += "  RTN_DM_SET(dm, " + std::to_string(k0 / 64) + ", " + std::to_string(k0 % 64) + " + (q" + id + " >> " +
+           std::to_string(run.shift) + "), " + reach + ");\n";
+  }
+
   void pc_flat(const PNode& n, const std::string& R) {
     bool first_unary = true;
     std::string T;
-    for (auto& c : n.children) {
+    for (size_t ci = 0; ci < n.children.size(); ++ci) {
+      const PNode& c = n.children[ci];
       if (!c.pred.on_packet()) continue;
+      if (range_runs && c.pred.is_binary()) {
+        const RangeRun run = range_run(n, ci, flat_pc_stmt);
+        if (run.len) {
+          pc_flat_range(n, ci, run, R, T, c.if_else);
+          ci += run.len - 1;
+          continue;
+        }
+      }
       const std::string id = std::to_string(c.id);
       std::string cond;
       bool is_else;
@@ -636,16 +734,19 @@ PacketProgram compile_packet_program(const std::vector<SubscriptionSpec>& subs) 
   prog.hip_body_branchy = "__device__ __forceinline__ void rtn_filter(const rtn_view& v, rtn_u32& act, rtn_u64* dm) {\n"
                           "  (void)v; (void)dm; RTN_KZ_DECL(v)\n" +
                           g.hip + "}\n";
-  g.hip.clear();
-  {
+  for (bool runs : {false, true}) {
+    g.hip.clear();
+    g.flat_pc_stmt = 0;
+    g.range_runs = runs;
     const std::string R0 = prog.wraps_ethernet ? "v.eth_ok" : "true";
     if (root_body) g.pc_flat_body(root, R0);
     g.pc_flat(root, R0);
     if (g.flat_pc_stmt != prog.delivers.size()) throw FilterError("internal: packet-continue statement count");
+    (runs ? prog.hip_body : prog.hip_body_chain) =
+        "__device__ __forceinline__ void rtn_filter(const rtn_view& v, rtn_u32& act, rtn_u64* dm) {\n"
+        "  (void)v; (void)dm; RTN_KZ_DECL(v)\n" +
+        g.hip + "}\n";
   }
-  prog.hip_body = "__device__ __forceinline__ void rtn_filter(const rtn_view& v, rtn_u32& act, rtn_u64* dm) {\n"
-                  "  (void)v; (void)dm; RTN_KZ_DECL(v)\n" +
-                  g.hip + "}\n";
   // The straight-line form evaluates every node for every frame; the nested form skips subtrees
   // no lane of a wave enters. Past kFlatMaxNodes the second wins (large disjoint subtrees).
   if (prog.tree.size > kFlatMaxNodes) prog.hip_body = prog.hip_body_branchy;
