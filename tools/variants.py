@@ -185,6 +185,21 @@ def kzdm(src: str) -> str:
 VARIANTS.update({"kz": kz, "kzdm": kzdm, "cpw2": cpw2, "chunk512": chunk512, "chunk128": chunk128, "rb128": rb128, "wpb2": wpb2})
 
 
+def nobarrel(src: str) -> str:
+    """Timing only: every wave takes the Eth/IPv4 constant-offset extraction (wrong views for
+    lanes with other offsets): the cost of the per-lane barrel shifter."""
+    return _sub(src, "    rtn_extract_v<NW>(w, q, v.l4off, v);", "    rtn_extract_c<NW, 14, 34>(w, v);")
+
+
+def nofilter(src: str) -> str:
+    """Timing only: the generated filter is replaced by "accept every IP frame, deliver one
+    statement on half of them" (a destination-address bit), keeping the output volume."""
+    return _sub(src, "  rtn_filter(v, act, dm);", "  act = (v.v4 || v.v6) ? 1u : 0u; dm[0] = (v.v4 || v.v6) ? (v.l3w[4] & 1u) : 0u;")
+
+
+VARIANTS.update({"nobarrel": nobarrel, "nofilter": nofilter})
+
+
 def write(name: str, outdir: Path) -> Path:
     """A variant file: a '+'-joined list of VARIANTS applied to the current kernel, or
     'file=<path>' (a kernel source as is, e.g. an older revision: git show REV:path > file)."""
