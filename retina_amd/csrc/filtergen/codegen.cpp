@@ -325,8 +325,34 @@ struct Gen {
   // lanes take different branches runs all of them anyway; this form drops the exec-mask
   // bookkeeping of each branch. Statement numbering follows children() / update_body().
   uint32_t flat_pc_stmt = 0;
+  // Actions folded into one flag per distinct action word, OR-ed over the reach flags of the
+  // nodes that carry it, and `act |= flag ? word : 0` once per word at the end (the
+  // RTN_FOLD_ACT experiment; the product form ORs each node's word under its flag).
+  bool fold_act = false;
+  std::map<uint32_t, std::string> act_flags;
+  void act_or(const PNode& n, const std::string& R) {
+    if (n.actions.drop()) return;
+    if (!fold_act) {
+      hip += "  act |= " + R + " ? " + u32lit(n.actions.data) + " : 0u;\n";
+      return;
+    }
+    auto it = act_flags.find(n.actions.data);
+    if (it == act_flags.end())
+      it = act_flags.emplace(n.actions.data, "a" + std::to_string(act_flags.size())).first;
+    hip += "  " + it->second + " = " + it->second + " || " + R + ";\n";
+  }
+  std::string act_prologue() const {
+    std::string s;
+    for (auto& kv : act_flags) s += "  bool " + kv.second + " = false;\n";
+    return s;
+  }
+  std::string act_epilogue() const {
+    std::string s;
+    for (auto& kv : act_flags) s += "  act |= " + kv.second + " ? " + u32lit(kv.first) + " : 0u;\n";
+    return s;
+  }
   void pc_flat_body(const PNode& n, const std::string& R) {
-    if (!n.actions.drop()) hip += "  act |= " + R + " ? " + u32lit(n.actions.data) + " : 0u;\n";
+    act_or(n, R);
     for (auto& dv : n.deliver) {
       uint32_t k = flat_pc_stmt++;
       if (k >= prog.delivers.size() || prog.delivers[k].sub_id != (uint32_t)dv.id)
@@ -417,9 +443,9 @@ struct Gen {
       hip += "  const bool " + rc + " = " + R + " && !" + T + " && k" + id + ";\n";
       hip += "  " + T + " = " + T + " || k" + id + ";\n";
     }
-    if (!first.actions.drop()) hip += "  act |= " + rc + " ? " + u32lit(first.actions.data) + " : 0u;\n";
+    act_or(first, rc);
     const std::string reach = prog.delivers[k0].payload ? "(" + rc + " && v.payload_ok)" : rc;
-    hip += "  RTN_DM_SET(dm, " + std::to_string(k0 / 64) + ", " + std::to_string(k0 % 64) + " + (q" + id + " >> " +
+    hip += "  RTN_DM_SETV(dm, " + std::to_string(k0 / 64) + ", " + std::to_string(k0 % 64) + " + (q" + id + " >> " +
            std::to_string(run.shift) + "), " + reach + ");\n";
   }
 
@@ -734,18 +760,20 @@ PacketProgram compile_packet_program(const std::vector<SubscriptionSpec>& subs) 
   prog.hip_body_branchy = "__device__ __forceinline__ void rtn_filter(const rtn_view& v, rtn_u32& act, rtn_u64* dm) {\n"
                           "  (void)v; (void)dm; RTN_KZ_DECL(v)\n" +
                           g.hip + "}\n";
-  for (bool runs : {false, true}) {
+  for (int form : {0, 1, 2}) {  // plain chain, range runs (the product), range runs + folded actions
     g.hip.clear();
     g.flat_pc_stmt = 0;
-    g.range_runs = runs;
+    g.act_flags.clear();
+    g.range_runs = form >= 1;
+    g.fold_act = form == 2;
     const std::string R0 = prog.wraps_ethernet ? "v.eth_ok" : "true";
     if (root_body) g.pc_flat_body(root, R0);
     g.pc_flat(root, R0);
     if (g.flat_pc_stmt != prog.delivers.size()) throw FilterError("internal: packet-continue statement count");
-    (runs ? prog.hip_body : prog.hip_body_chain) =
+    (form == 0 ? prog.hip_body_chain : form == 1 ? prog.hip_body : prog.hip_body_fold) =
         "__device__ __forceinline__ void rtn_filter(const rtn_view& v, rtn_u32& act, rtn_u64* dm) {\n"
         "  (void)v; (void)dm; RTN_KZ_DECL(v)\n" +
-        g.hip + "}\n";
+        g.act_prologue() + g.hip + g.act_epilogue() + "}\n";
   }
   // The straight-line form evaluates every node for every frame; the nested form skips subtrees
   // no lane of a wave enters. Past kFlatMaxNodes the second wins (large disjoint subtrees).

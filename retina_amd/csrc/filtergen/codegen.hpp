@@ -55,6 +55,7 @@ struct PacketProgram {
   std::string hip_body;     // __device__ function rtn_filter(...) specialised to this tree (straight-line)
   std::string hip_body_branchy;  // the same as nested if/else (RTN_BRANCHY_FILTER experiment)
   std::string hip_body_chain;    // straight-line without range runs (RTN_CHAIN_FILTER experiment)
+  std::string hip_body_fold;     // range runs + folded action flags (RTN_FOLD_ACT experiment)
   std::string rust_listing; // the Rust the reference filtergen would emit (normalised), for review
   bool wraps_ethernet = false;
   std::string hw_filter;    // get_hw_filter (filtergen/src/lib.rs:233-238): the NIC keep/drop filter

@@ -100,6 +100,8 @@ struct rtn_view {
 // Statement-mask bit b of word w, set under a node's reach flag r (the generated filters' only
 // form for delivery bits).
 #define RTN_DM_SET(m, w, b, r) ((m)[w] |= (r) ? (1ull << (b)) : 0ull)
+// ... and at a bit the lane computes (a range run's offset, codegen.cpp RangeRun).
+#define RTN_DM_SETV(m, w, b, r) ((m)[w] |= (r) ? (1ull << (b)) : 0ull)
 // Predicate constants of the generated filters are RTN_K(literal), and each filter body opens
 // with RTN_KZ_DECL(view): the identity and nothing here (tools/variants.py redefines them to time
 // constants that are not hoisted out of the group loop).

@@ -60,6 +60,7 @@ std::string build_source(const rtn::PacketProgram& prog) {
                      "#define RTN_PD_FACTS " + std::to_string(prog.pd_facts.size()) + "\n" + env_defines();
   const std::string& body = head.find("RTN_BRANCHY_FILTER") != std::string::npos ? prog.hip_body_branchy
                             : head.find("RTN_CHAIN_FILTER") != std::string::npos ? prog.hip_body_chain
+                            : head.find("RTN_FOLD_ACT") != std::string::npos     ? prog.hip_body_fold
                                                                                   : prog.hip_body;
   std::string src = head + tpl.substr(0, at) + body + tpl.substr(at + marker.size());
   const std::string cmarker = "//@@RTN_CONN_FILTER@@";

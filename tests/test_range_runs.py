@@ -38,7 +38,7 @@ def test_range_runs_emitted_where_they_apply():
     # child): 10.2-10.5 is a run, 10.0 alone is not; 255.255.255.250-255 (/32); under both ipv4
     # and ipv6: tcp.dst_port 8000-8009 and udp.src_port 104-107 (100-102 before the gap are too few)
     assert spans == sorted([64 << 8, 6 << 8, 4 << 16, 6, 10, 4, 10, 4]), spans
-    assert body.count("RTN_DM_SET(dm, 1, 0 + (q") == 1          # the word-1 remainder starts at bit 0
+    assert body.count("RTN_DM_SETV(dm, 1, 0 + (q") == 1          # the word-1 remainder starts at bit 0
     assert "v.payload_ok" in body
 
 

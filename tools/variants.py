@@ -200,6 +200,16 @@ def nofilter(src: str) -> str:
 VARIANTS.update({"nobarrel": nobarrel, "nofilter": nofilter})
 
 
+def dm32(src: str) -> str:
+    """Statement bits set on the 32-bit half that holds them (no 64-bit OR chain whose high
+    half ORs zeros)."""
+    return _sub(src, "#define RTN_DM_SET(m, w, b, r) ((m)[w] |= (r) ? (1ull << (b)) : 0ull)",
+                "#define RTN_DM_SET(m, w, b, r) (reinterpret_cast<rtn_u32*>(m)[2 * (w) + ((b) >> 5)] |= (r) ? (1u << ((b) & 31)) : 0u)")
+
+
+VARIANTS.update({"dm32": dm32})
+
+
 def write(name: str, outdir: Path) -> Path:
     """A variant file: a '+'-joined list of VARIANTS applied to the current kernel, or
     'file=<path>' (a kernel source as is, e.g. an older revision: git show REV:path > file)."""
