@@ -366,9 +366,10 @@ __device__ __forceinline__ rtn_u64 rtn_rec_slot(rtn_u64 nch, rtn_u64 c, rtn_u32 
 #define RTN_RING 128u
 #define RTN_FLUSH 64u
 
+template <bool CONN>
 __device__ __forceinline__ void rtn_flush(const rtn_args& a, const rtn_u64* ring, const rtn_u64* cring,
                                           const rtn_chunk& ch, rtn_u32 lane, rtn_u32 nrecs) {
-  if (a.flags & 4u) {
+  if (CONN) {
     // connection-stage entries (8 B) share the records' indices: same block, 128-B lines
     const rtn_u32 nc = ((nrecs + 1u) / 2u + 7u) & ~7u;
     // (a block of RTN_RB entries is RTN_RB / 2 lanes; a flush may span several blocks)
@@ -412,7 +413,7 @@ __device__ __forceinline__ void rtn_flush6(const rtn_args& a, const rtn_v4u* rin
 
 // Everything after the slot's bytes arrived: parse, generated filter, L4Context, wave-level
 // compaction of the outputs of group g (the k-th group of the current chunk).
-template <int NW, bool STAGE6>
+template <int NW, bool STAGE6, bool CONN>
 __device__ __forceinline__ void rtn_group(const rtn_args& a, rtn_u32 g, rtn_u32 k, rtn_u32 lane, rtn_u64 lane_lt,
                                           const rtn_u32 (&w)[NW], rtn_u32 dl, rtn_u64* ring, rtn_u64* cring,
                                           rtn_v4u* ring6, rtn_chunk& ch, rtn_acc& acc) {
@@ -461,7 +462,7 @@ __device__ __forceinline__ void rtn_group(const rtn_args& a, rtn_u32 g, rtn_u32 
     rp[0] = (rtn_u64)src4 | ((rtn_u64)dst4 << 32);
     rp[1] = (rtn_u64)ports | ((rtn_u64)seq << 32);
     rp[2] = (rtn_u64)ack | ((rtn_u64)meta << 32);
-    if (a.flags & 4u) {
+    if (CONN) {
       // Connection stage of the first packet (conntrack/mod.rs:80-169): ConnId, whether the frame
       // may open a connection (Conn::new_tcp / new_udp, conn/mod.rs:53-96) and the generated
       // packet_filter (ConnInfo::filter_first_packet, conn_info.rs:42-50) on this frame.
@@ -549,7 +550,7 @@ __device__ __forceinline__ void rtn_group(const rtn_args& a, rtn_u32 g, rtn_u32 
   }
   if (ch.nrec - ch.nflushed >= RTN_FLUSH) {  // pending < RTN_FLUSH + 64 <= RTN_RING: one block per group
     rtn_wave_sync();
-    rtn_flush(a, ring, cring, ch, lane, RTN_FLUSH);
+    rtn_flush<CONN>(a, ring, cring, ch, lane, RTN_FLUSH);
     ch.nflushed += RTN_FLUSH;
     rtn_wave_sync();
   }
@@ -582,7 +583,7 @@ __device__ __forceinline__ void rtn_group(const rtn_args& a, rtn_u32 g, rtn_u32 
 #define RTN_SPLIT 1
 #define RTN_MONO 2
 #define RTN_SPLITC 3
-template <int MODE>
+template <int MODE, bool CONN>
 __device__ __forceinline__ void rtn_run(const rtn_args& a) {
   const rtn_u32 lane = threadIdx.x & 63u;
   const rtn_u32 wave_g = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
@@ -594,7 +595,7 @@ __device__ __forceinline__ void rtn_run(const rtn_args& a) {
   rtn_acc acc = {0u, 0u, 0u, 0u, 0u, 0ull, 0ull, 0ull, 0ull};
   __shared__ __attribute__((aligned(16))) rtn_u64 rtn_ring[4][RTN_RING * 3u];
   rtn_u64* ring = rtn_ring[threadIdx.x >> 6];
-  __shared__ __attribute__((aligned(16))) rtn_u64 rtn_cring[4][RTN_RING];  // connection-stage entries
+  __shared__ __attribute__((aligned(16))) rtn_u64 rtn_cring[4][CONN ? RTN_RING : 2u];  // connection-stage entries
   rtn_u64* cring = rtn_cring[threadIdx.x >> 6];
   constexpr bool stage6 = MODE != RTN_S64;  // 64-byte slots rarely forward IPv6 (only short UDP)
   __shared__ __attribute__((aligned(16))) rtn_v4u rtn_ring6[4][stage6 ? RTN_RING6 * 2u : 1u];
@@ -637,7 +638,7 @@ __device__ __forceinline__ void rtn_run(const rtn_args& a) {
         rtn_load_lo(a, g * 64u + lane, lo, dl);
       }
       if (MODE == RTN_S64) {
-        rtn_group<16, stage6>(a, g, g - gb, lane, lane_lt, lo, dl, ring, cring, ring6, ch, acc);
+        rtn_group<16, stage6, CONN>(a, g, g - gb, lane, lane_lt, lo, dl, ring, cring, ring6, ch, acc);
       } else {
         rtn_u32 w[32];
 #pragma unroll
@@ -667,12 +668,12 @@ __device__ __forceinline__ void rtn_run(const rtn_args& a) {
             w[16 + 4 * j + 0] = x.x; w[16 + 4 * j + 1] = x.y; w[16 + 4 * j + 2] = x.z; w[16 + 4 * j + 3] = x.w;
           }
         }
-        rtn_group<32, stage6>(a, g, g - gb, lane, lane_lt, w, dl, ring, cring, ring6, ch, acc);
+        rtn_group<32, stage6, CONN>(a, g, g - gb, lane, lane_lt, w, dl, ring, cring, ring6, ch, acc);
       }
     }
     // chunk epilogue: the partial last record block, then one store per bitmap for the chunk
     rtn_wave_sync();
-    rtn_flush(a, ring, cring, ch, lane, ch.nrec - ch.nflushed);
+    rtn_flush<CONN>(a, ring, cring, ch, lane, ch.nrec - ch.nflushed);
     if (stage6) rtn_flush6(a, ring6, ch, lane, ch.nv6 - ch.nv6flushed);
     rtn_wave_sync();
     if (lane < ge - gb) {
@@ -709,10 +710,18 @@ __device__ __forceinline__ void rtn_run(const rtn_args& a) {
   }
 }
 
-extern "C" __global__ void __launch_bounds__(256) rtn_pc_kernel(rtn_args a) { rtn_run<RTN_MONO>(a); }
-extern "C" __global__ void __launch_bounds__(256) rtn_pc_kernel_s64(rtn_args a) { rtn_run<RTN_S64>(a); }
-extern "C" __global__ void __launch_bounds__(256) rtn_pc_kernel_split(rtn_args a) { rtn_run<RTN_SPLIT>(a); }
-extern "C" __global__ void __launch_bounds__(256) rtn_pc_kernel_splitc(rtn_args a) { rtn_run<RTN_SPLITC>(a); }
+// One instance per slot layout, each with and without the connection stage (rtn_pc_out_t.conn):
+// compiled out, the stage's code and its LDS ring no longer hold registers and LDS the plain
+// packet stage needs (cfg4's compact split kernel: 134 -> 121 VGPRs, 3 -> 4 waves per SIMD, SGPR
+// spills 68 -> 40).
+extern "C" __global__ void __launch_bounds__(256) rtn_pc_kernel(rtn_args a) { rtn_run<RTN_MONO, false>(a); }
+extern "C" __global__ void __launch_bounds__(256) rtn_pc_kernel_s64(rtn_args a) { rtn_run<RTN_S64, false>(a); }
+extern "C" __global__ void __launch_bounds__(256) rtn_pc_kernel_split(rtn_args a) { rtn_run<RTN_SPLIT, false>(a); }
+extern "C" __global__ void __launch_bounds__(256) rtn_pc_kernel_splitc(rtn_args a) { rtn_run<RTN_SPLITC, false>(a); }
+extern "C" __global__ void __launch_bounds__(256) rtn_pc_kernel_conn(rtn_args a) { rtn_run<RTN_MONO, true>(a); }
+extern "C" __global__ void __launch_bounds__(256) rtn_pc_kernel_s64_conn(rtn_args a) { rtn_run<RTN_S64, true>(a); }
+extern "C" __global__ void __launch_bounds__(256) rtn_pc_kernel_split_conn(rtn_args a) { rtn_run<RTN_SPLIT, true>(a); }
+extern "C" __global__ void __launch_bounds__(256) rtn_pc_kernel_splitc_conn(rtn_args a) { rtn_run<RTN_SPLITC, true>(a); }
 
 // ---------------------------------------------------------------------------------------------
 // PacketDeliver filter (rtn_pd_run): the generated `packet_deliver` (filtergen/src/lib.rs:357-362,

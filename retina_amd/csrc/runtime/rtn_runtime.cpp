@@ -280,12 +280,14 @@ struct rtn_pc {
   hipFunction_t fn_s64 = nullptr;    // rtn_pc_kernel_s64: 64-byte slots
   hipFunction_t fn_split = nullptr;  // rtn_pc_kernel_split: 64-byte slots + ext
   hipFunction_t fn_splitc = nullptr; // rtn_pc_kernel_splitc: 64-byte slots + compact ext rows
+  hipFunction_t fn_conn[4] = {};     // the same four with the connection stage (*_conn), same order
   hipFunction_t fn_pd = nullptr;     // rtn_pd_kernel: the PacketDeliver filter (rtn_pd_run)
   hipFunction_t fn_idx[3] = {};      // rtn_idx_count / rtn_idx_scan / rtn_idx_write (rtn_pc_index)
   uint32_t* idx_block_sum = nullptr; // their per-block sums (RTN_MAX_FRAMES / 64 / RTN_IDX_WORDS)
   uint32_t blocks = 0;
   uint32_t threads = 256;  // threads per block of the packet kernel (4 waves, one chunk each)
   uint32_t splitc_cpw = 1;  // chunks per wave of rtn_pc_kernel_splitc (rtn_args.cpw)
+  uint32_t splitc_cpw_conn = 1;  // ... of rtn_pc_kernel_splitc_conn
   // used when the caller passes no counters: word RTN_CNT_STATUS accumulates the status bits of
   // such runs until rtn_pc_take_status reads and clears them (the other words are never read)
   uint32_t* scratch_counters = nullptr;
@@ -496,17 +498,31 @@ int32_t rtn_pc_create_from_program(rtn_program_t* p, int device, rtn_pc_t** out)
   e = hipModuleGetFunction(&pc->fn_splitc, pc->module, "rtn_pc_kernel_splitc");
   if (e != hipSuccess) return fail(RTN_EDEVICE, std::string("hipModuleGetFunction: ") + hipGetErrorString(e));
   {
-    // two consecutive chunks per wave when the compact split kernel's VGPRs hold it below 4
-    // waves per SIMD (its LDS allows 4): see the chunk loop in pc_kernel.hip
+    const char* names[4] = {"rtn_pc_kernel_conn", "rtn_pc_kernel_s64_conn", "rtn_pc_kernel_split_conn",
+                            "rtn_pc_kernel_splitc_conn"};
+    for (int k = 0; k < 4; ++k) {
+      e = hipModuleGetFunction(&pc->fn_conn[k], pc->module, names[k]);
+      if (e != hipSuccess) return fail(RTN_EDEVICE, std::string("hipModuleGetFunction: ") + hipGetErrorString(e));
+    }
+  }
+  // two consecutive chunks per wave when the compact split kernel's VGPRs hold it below 4 waves
+  // per SIMD (its LDS allows 4): see the chunk loop in pc_kernel.hip
+  auto cpw_for = [](hipFunction_t f, const char* name) {
     int vgprs = 0;
-    if (hipFuncGetAttribute(&vgprs, HIP_FUNC_ATTRIBUTE_NUM_REGS, pc->fn_splitc) == hipSuccess && vgprs > 0) {
+    uint32_t cpw = 1;
+    if (hipFuncGetAttribute(&vgprs, HIP_FUNC_ATTRIBUTE_NUM_REGS, f) == hipSuccess && vgprs > 0) {
       const int regs = (vgprs + 7) / 8 * 8;  // allocation granule
-      pc->splitc_cpw = 512 / regs < 4 ? 2u : 1u;
+      cpw = 512 / regs < 4 ? 2u : 1u;
     }
 #ifdef RTN_EXPERIMENTS
-    if (getenv("RTN_DEBUG")) fprintf(stderr, "rtn_pc_kernel_splitc: %d VGPRs, %u chunks per wave\n", vgprs, pc->splitc_cpw);
+    if (getenv("RTN_DEBUG")) fprintf(stderr, "%s: %d VGPRs, %u chunks per wave\n", name, vgprs, cpw);
+#else
+    (void)name;
 #endif
-  }
+    return cpw;
+  };
+  pc->splitc_cpw = cpw_for(pc->fn_splitc, "rtn_pc_kernel_splitc");
+  pc->splitc_cpw_conn = cpw_for(pc->fn_conn[3], "rtn_pc_kernel_splitc_conn");
   e = hipModuleGetFunction(&pc->fn_pd, pc->module, "rtn_pd_kernel");
   if (e != hipSuccess) return fail(RTN_EDEVICE, std::string("hipModuleGetFunction: ") + hipGetErrorString(e));
   {
@@ -525,7 +541,7 @@ int32_t rtn_pc_create_from_program(rtn_program_t* p, int device, rtn_pc_t** out)
 #ifdef RTN_EXPERIMENTS
   if (const char* g = getenv("RTN_GRID")) pc->blocks = (uint32_t)strtoul(g, nullptr, 10);
   if (const char* b = getenv("RTN_BLOCK")) pc->threads = (uint32_t)strtoul(b, nullptr, 10);
-  if (const char* c = getenv("RTN_CPW")) pc->splitc_cpw = (uint32_t)strtoul(c, nullptr, 10);
+  if (const char* c = getenv("RTN_CPW")) pc->splitc_cpw = pc->splitc_cpw_conn = (uint32_t)strtoul(c, nullptr, 10);
 #endif
   *out = pc.release();
   return RTN_OK;
@@ -591,7 +607,7 @@ int32_t rtn_pc_run(rtn_pc_t* pc, const rtn_batch_t* in, rtn_pc_out_t* out, void*
             ((in->flags & RTN_BATCH_DL_LE64) ? 8u : 0u) | ((in->flags & RTN_BATCH_EXT_COMPACT) ? 16u : 0u);
   a.ext_chunk = in->ext_chunk;
   a.ext_rows = in->ext_rows;
-  a.cpw = (in->ext && (in->flags & RTN_BATCH_EXT_COMPACT)) ? pc->splitc_cpw : 1u;
+  a.cpw = (in->ext && (in->flags & RTN_BATCH_EXT_COMPACT)) ? (out->conn ? pc->splitc_cpw_conn : pc->splitc_cpw) : 1u;
   a.pc_bm = out->pc_bitmap;
   a.fwd_bm = out->fwd_bitmap;
   a.recs = out->l4;
@@ -614,8 +630,9 @@ int32_t rtn_pc_run(rtn_pc_t* pc, const rtn_batch_t* in, rtn_pc_out_t* out, void*
 #endif
   if (blocks == 0) blocks = 1;
   void* params[] = {&a};
-  hipFunction_t fn = in->ext ? ((in->flags & RTN_BATCH_EXT_COMPACT) ? pc->fn_splitc : pc->fn_split)
-                             : (in->stride == 64 ? pc->fn_s64 : pc->fn);
+  const int layout = in->ext ? ((in->flags & RTN_BATCH_EXT_COMPACT) ? 3 : 2) : (in->stride == 64 ? 1 : 0);
+  const hipFunction_t plain[4] = {pc->fn, pc->fn_s64, pc->fn_split, pc->fn_splitc};
+  hipFunction_t fn = out->conn ? pc->fn_conn[layout] : plain[layout];
   e = hipModuleLaunchKernel(fn, blocks, 1, 1, threads, 1, 1, 0, s, params, nullptr);
   if (e != hipSuccess) return fail(RTN_EDEVICE, std::string("hipModuleLaunchKernel: ") + hipGetErrorString(e));
   return RTN_OK;

@@ -29,10 +29,10 @@ def ceiling(src: str) -> str:
   }
   if (x == 0x9E3779B9u) a.counters[3] = x;
 }'''
-    for k in ("rtn_pc_kernel(rtn_args a) { rtn_run<RTN_MONO>(a); }",
-              "rtn_pc_kernel_s64(rtn_args a) { rtn_run<RTN_S64>(a); }",
-              "rtn_pc_kernel_split(rtn_args a) { rtn_run<RTN_SPLIT>(a); }",
-              "rtn_pc_kernel_splitc(rtn_args a) { rtn_run<RTN_SPLITC>(a); }"):
+    for k in ("rtn_pc_kernel(rtn_args a) { rtn_run<RTN_MONO, false>(a); }",
+              "rtn_pc_kernel_s64(rtn_args a) { rtn_run<RTN_S64, false>(a); }",
+              "rtn_pc_kernel_split(rtn_args a) { rtn_run<RTN_SPLIT, false>(a); }",
+              "rtn_pc_kernel_splitc(rtn_args a) { rtn_run<RTN_SPLITC, false>(a); }"):
         src = _sub(src, k, k.split(" {")[0] + " " + body)
     return src
 
@@ -42,7 +42,7 @@ def nostores(src: str) -> str:
     src = _sub(src, "  if (fwd) {\n    const rtn_u32 r", "  if (fwd && a.n == 0u) {\n    const rtn_u32 r")
     src = _sub(src, "    if (d) {", "    if (d && a.n == 0u) {")
     src = _sub(src, "  const bool six = fwd && v.v6 && (a.flags & 1u);", "  const bool six = false;")
-    src = _sub(src, "    rtn_flush(a, ring, cring, ch, lane, ch.nrec - ch.nflushed);", "")
+    src = _sub(src, "    rtn_flush<CONN>(a, ring, cring, ch, lane, ch.nrec - ch.nflushed);", "")
     src = _sub(src, "  if (ch.nrec - ch.nflushed >= RTN_FLUSH) {", "  if (false) {")
     return src
 
@@ -84,11 +84,6 @@ def tstores(src: str) -> str:
     return _sub(src, "#define RTN_ST(p, v) __builtin_nontemporal_store((v), (p))", "#define RTN_ST(p, v) (*(p) = (v))")
 
 
-def noconn(src: str) -> str:
-    """Timing only: the connection-stage code compiled out (register pressure without it)."""
-    return src.replace("if (a.flags & 4u) {", "if (false) {")
-
-
 def _store_asm(mods: str):
     def v(src: str) -> str:
         return _sub(src, "#define RTN_ST(p, v) __builtin_nontemporal_store((v), (p))",
@@ -108,8 +103,8 @@ def dm_opq(src: str) -> str:
 
 def oldform(src: str) -> str:
     """The compact ext path as a run-time branch of the split kernel instance (round-2 form)."""
-    src = _sub(src, "rtn_pc_kernel_splitc(rtn_args a) { rtn_run<RTN_SPLITC>(a); }",
-               "rtn_pc_kernel_splitc(rtn_args a) { rtn_run<RTN_SPLIT>(a); }")
+    src = _sub(src, "rtn_pc_kernel_splitc(rtn_args a) { rtn_run<RTN_SPLITC, false>(a); }",
+               "rtn_pc_kernel_splitc(rtn_args a) { rtn_run<RTN_SPLIT, false>(a); }")
     return _sub(src, "        if (MODE == RTN_SPLITC) {\n          const rtn_u64 nm = __ballot(need);",
                 "        if (MODE == RTN_SPLIT && (a.flags & 16u)) {\n          const rtn_u64 nm = __ballot(need);")
 
@@ -126,7 +121,7 @@ def splitc_pf(src: str) -> str:
 
 
 VARIANTS.update({"oldform": oldform, "splitc_w4": splitc_w4, "splitc_pf": splitc_pf, "dm_opq": dm_opq, "dense": dense, "nobitmaps": nobitmaps, "bm128": bm128, "noext": noext, "tstores": tstores,
-                 "noconn": noconn, "st_sc1": _store_asm("sc1"), "st_sc0sc1": _store_asm("sc0 sc1"),
+                 "st_sc1": _store_asm("sc1"), "st_sc0sc1": _store_asm("sc0 sc1"),
                  "st_ntsc1": _store_asm("nt sc1"), "st_nt": _store_asm("nt")})
 
 
@@ -154,15 +149,6 @@ def wpb2(src: str) -> str:
     return src
 
 
-def cpw2(src: str) -> str:
-    """The compact split kernel walks two consecutive chunks per wave (a 512-frame work unit over
-    the 256-frame layout); @GRID = ceil(n / 2048)."""
-    return _sub(src, "  for (rtn_u32 c = wave_g; c < nchunks; c += nwaves) {",
-                "  constexpr rtn_u32 CPW = MODE == RTN_SPLITC ? 2u : 1u;\n"
-                "  for (rtn_u32 cw = wave_g * CPW; cw < nchunks; cw += nwaves * CPW)\n"
-                "  for (rtn_u32 c = cw; c < cw + CPW && c < nchunks; ++c) {")
-
-
 def kz(src: str) -> str:
     """Predicate constants XORed with a per-group run-time zero (readfirstlane(nrec >> 31)) so that
     the compiler cannot hoist them out of the group loop into SGPRs (cfg4: 72 SGPR spills)."""
@@ -182,7 +168,7 @@ def kzdm(src: str) -> str:
                 "#define RTN_DM_SET(m, w, b, r) ((m)[w] |= (r) ? ((1ull << (b)) ^ (rtn_u64)rtn_kz) : 0ull)")
 
 
-VARIANTS.update({"kz": kz, "kzdm": kzdm, "cpw2": cpw2, "chunk512": chunk512, "chunk128": chunk128, "rb128": rb128, "wpb2": wpb2})
+VARIANTS.update({"kz": kz, "kzdm": kzdm, "chunk512": chunk512, "chunk128": chunk128, "rb128": rb128, "wpb2": wpb2})
 
 
 def nobarrel(src: str) -> str:
@@ -208,6 +194,18 @@ def dm32(src: str) -> str:
 
 
 VARIANTS.update({"dm32": dm32})
+
+
+def withconn(src: str) -> str:
+    """The kernels without the connection stage compiled as before its specialisation: the stage's
+    code and LDS ring present, skipped at run time (flags bit 2)."""
+    src = src.replace("if (CONN) {", "if (CONN && (a.flags & 4u)) {")
+    for m in ("RTN_MONO", "RTN_S64", "RTN_SPLIT", "RTN_SPLITC"):
+        src = _sub(src, f"{{ rtn_run<{m}, false>(a); }}", f"{{ rtn_run<{m}, true>(a); }}")
+    return src
+
+
+VARIANTS.update({"withconn": withconn})
 
 
 def write(name: str, outdir: Path) -> Path:
