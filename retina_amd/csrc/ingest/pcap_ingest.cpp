@@ -43,6 +43,7 @@ struct rtn_pcap {
   uint32_t mtu = 0;
   rtn_pcap_stats_t st{};
   size_t populated = 0;  // page tables mapped up to here (prefault)
+  size_t prefetched = 0; // cache lines requested up to here (prefetch_ahead)
 };
 
 namespace {
@@ -63,6 +64,22 @@ void prefault(rtn_pcap* p, size_t off, size_t bytes) {
   (void)off;
   (void)bytes;
 #endif
+}
+
+// The walk is a chain of dependent loads (each record header's offset comes from the previous
+// one's length), one cache miss per record on captures of full-size frames. Records are
+// contiguous, so the lines a few KB ahead of the walk will be read whatever their record
+// boundaries: requesting them early turns the chain of misses into a stream (IMIX capture,
+// 2^21 frames: 16.4 -> 27 Mpkt/s packed into the compact split layout, this container).
+// Captures of small frames are read line after line anyway; the prefetch runs once the mean
+// frame seen so far is long enough to skip lines.
+constexpr size_t kPrefetchAhead = 4096;
+constexpr uint64_t kPrefetchMinMean = 192;
+inline void prefetch_ahead(rtn_pcap* p) {
+  if (p->st.packed < 64 || p->st.bytes < kPrefetchMinMean * p->st.packed) return;
+  const size_t end = p->off + kPrefetchAhead < p->size ? p->off + kPrefetchAhead : p->size;
+  if (p->prefetched < p->off) p->prefetched = p->off & ~size_t(63);
+  for (; p->prefetched < end; p->prefetched += 64) __builtin_prefetch(p->base + p->prefetched);
 }
 
 // Next frame of the capture: captured bytes + original length. Returns false at end of file
@@ -160,6 +177,7 @@ int32_t rtn_pcap_next_batch(rtn_pcap_t* p, uint8_t* slab, uint64_t stride, uint1
     const uint8_t* data;
     uint32_t caplen, origlen;
     const size_t at = p->off;
+    prefetch_ahead(p);
     if (!next_frame(p, data, caplen, origlen)) break;
     p->st.frames++;
     if (origlen > p->mtu) {  // offline.rs:68-70
@@ -191,6 +209,7 @@ int32_t rtn_pcap_next_batch_split(rtn_pcap_t* p, uint8_t* head, uint8_t* ext, ui
     const uint8_t* data;
     uint32_t caplen, origlen;
     const size_t at = p->off;
+    prefetch_ahead(p);
     if (!next_frame(p, data, caplen, origlen)) break;
     p->st.frames++;
     if (origlen > p->mtu) {  // offline.rs:68-70
@@ -238,6 +257,7 @@ int32_t rtn_pcap_stats(const rtn_pcap_t* p, rtn_pcap_stats_t* st) {
 int32_t rtn_pcap_rewind(rtn_pcap_t* p) {
   if (!p) return rtn::set_error(RTN_EINVAL, "null argument");
   p->off = p->first;
+  p->prefetched = 0;
   if (p->fmt == Fmt::Pcapng) p->swap = false;
   return RTN_OK;
 }
