@@ -329,7 +329,7 @@ struct Gen {
   // nodes that carry it, and `act |= flag ? word : 0` once per word at the end (the
   // RTN_FOLD_ACT experiment; the product form ORs each node's word under its flag).
   bool fold_act = false;
-  std::map<uint32_t, std::string> act_flags;
+  std::map<uint32_t, std::string> act_flags{};
   void act_or(const PNode& n, const std::string& R) {
     if (n.actions.drop()) return;
     if (!fold_act) {
