@@ -65,6 +65,12 @@ def test_hiprtc_builds_gfx950_code_object(fset):
     co = pc.Program.from_spec(SETS[fset]).code_object()
     assert len(co) > 1000
     assert b"gfx950" in co or co[:4] == b"\x7fELF" or co[:24].startswith(b"__CLANG_OFFLOAD_BUNDLE__")
+    # every entry point rtn_pc_create looks up (rtn_runtime.cpp): four slot layouts, each with and
+    # without the connection stage, the PacketDeliver filter and the index kernels
+    for name in ("rtn_pc_kernel", "rtn_pc_kernel_s64", "rtn_pc_kernel_split", "rtn_pc_kernel_splitc",
+                 "rtn_pd_kernel", "rtn_idx_count", "rtn_idx_scan", "rtn_idx_write"):
+        for sym in (name, name + "_conn") if name.startswith("rtn_pc_kernel") else (name,):
+            assert (sym + ".kd").encode() in co, sym
 
 
 def test_output_sizes():
