@@ -400,14 +400,18 @@ __device__ __forceinline__ void rtn_flush(const rtn_args& a, const rtn_u64* ring
 #define RTN_RING6 64u
 #define RTN_FLUSH6 32u
 
+// Stores ring entries [nv6flushed, nv6flushed + nent) (nent <= RTN_RING6), rounded up to whole
+// 128-B lines (4 entries): a partial line costs a read-modify-write. Only a chunk's last store is
+// partial, and its padding (stale ring bytes) lands in the chunk's unused addr6 space, as for the
+// record blocks.
 __device__ __forceinline__ void rtn_flush6(const rtn_args& a, const rtn_v4u* ring6, const rtn_chunk& ch, rtn_u32 lane,
                                            rtn_u32 nent) {
-  const rtn_v4u* src = ring6 + (ch.nv6flushed & (RTN_RING6 - 1u)) * 2u;
+  const rtn_u32 nv4 = ((nent + 3u) & ~3u) * 2u;  // 16-B halves
   rtn_v4u* dst = reinterpret_cast<rtn_v4u*>(a.addr6 + (ch.rec_base + ch.nv6flushed) * 32u);
 #pragma unroll
   for (rtn_u32 j = 0; j < 2u; ++j) {
     const rtn_u32 k = lane + 64u * j;
-    if (k < 2u * nent) RTN_ST(dst + k, src[k]);
+    if (k < nv4) RTN_ST(dst + k, ring6[((ch.nv6flushed + k / 2u) & (RTN_RING6 - 1u)) * 2u + (k & 1u)]);
   }
 }
 
@@ -528,25 +532,44 @@ __device__ __forceinline__ void rtn_group(const rtn_args& a, rtn_u32 g, rtn_u32 
   // IPv6 source/destination addresses, ranked among the chunk's forwarded IPv6 frames
   const bool six = fwd && v.v6 && (a.flags & 1u);
   const rtn_u64 m6 = __ballot(six);
-  if (six) {
-    const rtn_u32 r6 = ch.nv6 + (rtn_u32)__popcll(m6 & lane_lt);
-    const rtn_v4u s0 = rtn_v4u{v.l3w[2], v.l3w[3], v.l3w[4], v.l3w[5]};
-    const rtn_v4u s1 = rtn_v4u{v.l3w[6], v.l3w[7], v.l3w[8], v.l3w[9]};
-    if (STAGE6) {
+  const rtn_u32 rank6 = (rtn_u32)__popcll(m6 & lane_lt), cnt6 = (rtn_u32)__popcll(m6);
+  const rtn_u32 r6 = ch.nv6 + rank6;
+  const rtn_v4u s0 = rtn_v4u{v.l3w[2], v.l3w[3], v.l3w[4], v.l3w[5]};
+  const rtn_v4u s1 = rtn_v4u{v.l3w[6], v.l3w[7], v.l3w[8], v.l3w[9]};
+  if (STAGE6) {
+    // Fewer than RTN_FLUSH6 entries are pending when a group starts (drained below), so at least
+    // RTN_RING6 - RTN_FLUSH6 + 1 of the group's (at most 64) entries have a free ring slot. In an
+    // IPv6-dense group the rest wait until one block has been stored.
+    const rtn_u32 room = RTN_RING6 - (ch.nv6 - ch.nv6flushed);
+    if (six && rank6 < room) {
       ring6[(r6 & (RTN_RING6 - 1u)) * 2u] = s0;
       ring6[(r6 & (RTN_RING6 - 1u)) * 2u + 1u] = s1;
-    } else {
+    }
+    if (cnt6 > room) {
+      rtn_wave_sync();
+      rtn_flush6(a, ring6, ch, lane, RTN_FLUSH6);
+      ch.nv6flushed += RTN_FLUSH6;
+      rtn_wave_sync();
+      if (six && rank6 >= room) {
+        ring6[(r6 & (RTN_RING6 - 1u)) * 2u] = s0;
+        ring6[(r6 & (RTN_RING6 - 1u)) * 2u + 1u] = s1;
+      }
+    }
+    ch.nv6 += cnt6;
+    if (ch.nv6 - ch.nv6flushed >= RTN_FLUSH6) {  // every whole block pending (at most 64 entries)
+      const rtn_u32 nb = (ch.nv6 - ch.nv6flushed) & ~(RTN_FLUSH6 - 1u);
+      rtn_wave_sync();
+      rtn_flush6(a, ring6, ch, lane, nb);
+      ch.nv6flushed += nb;
+      rtn_wave_sync();
+    }
+  } else {
+    if (six) {
       rtn_v4u* ap = reinterpret_cast<rtn_v4u*>(a.addr6 + (ch.rec_base + r6) * 32u);
       ap[0] = s0;
       ap[1] = s1;
     }
-  }
-  ch.nv6 += (rtn_u32)__popcll(m6);
-  if (STAGE6 && ch.nv6 - ch.nv6flushed >= RTN_FLUSH6) {
-    rtn_wave_sync();
-    rtn_flush6(a, ring6, ch, lane, RTN_FLUSH6);
-    ch.nv6flushed += RTN_FLUSH6;
-    rtn_wave_sync();
+    ch.nv6 += cnt6;
   }
   if (ch.nrec - ch.nflushed >= RTN_FLUSH) {  // pending < RTN_FLUSH + 64 <= RTN_RING: one block per group
     rtn_wave_sync();

@@ -291,3 +291,23 @@ def test_outputs_in_mapped_host_memory(gpu):
     assert np.array_equal(a["fwd"], b["fwd"]) and np.array_equal(a["l4"], b["l4"])
     assert np.array_equal(a["addr6"], b["addr6"])
     assert int(b["fwd"].sum()) > n // 2
+
+
+@pytest.mark.parametrize("layout", [False, True, "compact"])
+def test_ipv6_dense_batches(layout, gpu):
+    """Runs of groups where (almost) every frame is a forwarded IPv6 frame: the IPv6 address
+    records of a chunk pass through the per-wave LDS ring faster than one block per group, so the
+    ring must be drained before it wraps onto records not yet stored (pc_kernel.hip rtn_group)."""
+    rng = np.random.default_rng(66)
+    frames = []
+    for j in range(9 * 256 + 77):
+        v6 = (j // 256) % 3 != 2 or rng.random() < 0.5   # two all-IPv6 chunks, then a mixed one
+        proto = 6 if rng.random() < 0.8 else 17
+        src = int(rng.integers(0, 1 << 62)) << 66 | j if v6 else int(rng.integers(0, 1 << 32))
+        dst = int(rng.integers(0, 1 << 62)) << 66 | (j * 7) if v6 else int(rng.integers(0, 1 << 32))
+        frames.append(helpers.build_frame(v6, src, dst, int(rng.integers(1, 65536)), int(rng.integers(1, 65536)),
+                                          proto, 0x18, payload=bytes(int(rng.integers(0, 9)))))
+    slab, dlen = pc.pack_frames(frames, 128)
+    spec = synth._toml([("tcp or udp", ["ConnRecord"], "all"), ("ipv6.src_addr = ::/0 and tcp", ["ZcFrame"], "z6")])
+    helpers.assert_same(helpers.gpu_run(spec, slab, 128, dlen, split=layout),
+                        helpers.oracle_run(spec, slab, 128, dlen), f"ipv6 dense/{layout}")
