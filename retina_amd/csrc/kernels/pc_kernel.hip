@@ -394,10 +394,13 @@ __device__ __forceinline__ void rtn_flush(const rtn_args& a, const rtn_u64* ring
 
 // IPv6 address records (32 B: src, dst) are dense per chunk over the chunk's forwarded IPv6
 // frames. Where IPv6 is common (the split / wide-slot kernels) they leave through their own
-// per-wave LDS ring (64 entries, 2 KB) in whole 1-KB blocks: scattered 32-B stores with holes
-// between them cost about 4x their bytes in HBM time. (A 128-entry ring, 2-KB blocks, holds the
-// block to 3 per CU by LDS: cfg4 0.2028 -> 0.1942 ms with 64, in-process A/B.)
-#define RTN_RING6 64u
+// per-wave LDS ring (96 entries, 3 KB) in whole 1-KB blocks: scattered 32-B stores with holes
+// between them cost about 4x their bytes in HBM time. A group adds up to 64 entries, so the ring
+// holds them on top of the < 32 a group starts with. (A 128-entry ring holds the block to 3 per
+// CU by LDS: cfg4 0.2028 -> 0.1942 ms with 64, in-process A/B; 96 keeps 4 now that the packet
+// stage without the connection stage has no conn ring. A 64-entry ring needs a second store pass
+// in IPv6-dense groups: cfg3 +2 %.)
+#define RTN_RING6 96u
 #define RTN_FLUSH6 32u
 
 // Stores ring entries [nv6flushed, nv6flushed + nent) (nent <= RTN_RING6), rounded up to whole
@@ -411,7 +414,7 @@ __device__ __forceinline__ void rtn_flush6(const rtn_args& a, const rtn_v4u* rin
 #pragma unroll
   for (rtn_u32 j = 0; j < 2u; ++j) {
     const rtn_u32 k = lane + 64u * j;
-    if (k < nv4) RTN_ST(dst + k, ring6[((ch.nv6flushed + k / 2u) & (RTN_RING6 - 1u)) * 2u + (k & 1u)]);
+    if (k < nv4) RTN_ST(dst + k, ring6[((ch.nv6flushed + k / 2u) % RTN_RING6) * 2u + (k & 1u)]);
   }
 }
 
@@ -537,23 +540,11 @@ __device__ __forceinline__ void rtn_group(const rtn_args& a, rtn_u32 g, rtn_u32 
   const rtn_v4u s0 = rtn_v4u{v.l3w[2], v.l3w[3], v.l3w[4], v.l3w[5]};
   const rtn_v4u s1 = rtn_v4u{v.l3w[6], v.l3w[7], v.l3w[8], v.l3w[9]};
   if (STAGE6) {
-    // Fewer than RTN_FLUSH6 entries are pending when a group starts (drained below), so at least
-    // RTN_RING6 - RTN_FLUSH6 + 1 of the group's (at most 64) entries have a free ring slot. In an
-    // IPv6-dense group the rest wait until one block has been stored.
-    const rtn_u32 room = RTN_RING6 - (ch.nv6 - ch.nv6flushed);
-    if (six && rank6 < room) {
-      ring6[(r6 & (RTN_RING6 - 1u)) * 2u] = s0;
-      ring6[(r6 & (RTN_RING6 - 1u)) * 2u + 1u] = s1;
-    }
-    if (cnt6 > room) {
-      rtn_wave_sync();
-      rtn_flush6(a, ring6, ch, lane, RTN_FLUSH6);
-      ch.nv6flushed += RTN_FLUSH6;
-      rtn_wave_sync();
-      if (six && rank6 >= room) {
-        ring6[(r6 & (RTN_RING6 - 1u)) * 2u] = s0;
-        ring6[(r6 & (RTN_RING6 - 1u)) * 2u + 1u] = s1;
-      }
+    // Fewer than RTN_FLUSH6 entries are pending when a group starts (every whole block is stored
+    // below), so the group's at most 64 entries always find free slots in the 96-entry ring.
+    if (six) {
+      ring6[(r6 % RTN_RING6) * 2u] = s0;
+      ring6[(r6 % RTN_RING6) * 2u + 1u] = s1;
     }
     ch.nv6 += cnt6;
     if (ch.nv6 - ch.nv6flushed >= RTN_FLUSH6) {  // every whole block pending (at most 64 entries)
