@@ -628,13 +628,17 @@ __device__ __forceinline__ void rtn_run(const rtn_args& a) {
     // compact ext: the chunk's first row, read once per chunk (its latency overlaps the first
     // group's loads; read per group it was a dependent round trip in every group)
     const rtn_u32 xrow0 = MODE == RTN_SPLITC ? a.ext_chunk[c] : 0u;
-    // 64-byte slots without ext: the next group's loads are issued before this group is parsed,
-    // so one group of loads is always in flight per wave (cfg2 -2.2 %, in-process A/B; with the
-    // split layout's dependent ext loads it measured 5 % slower on cfg4 and is not used there)
+    // 64-byte slots without ext: the loads of the next two groups are issued before this group is
+    // parsed, so two groups of loads are in flight per wave (one group ahead: cfg2 -2.2 %, two:
+    // -0.4 % more, in-process A/B; with the split layout's dependent ext loads one group ahead
+    // measured 5 % slower on cfg4 and is not used there)
     constexpr bool prefetch = MODE == RTN_S64;
-    rtn_v4u qn[4];
-    rtn_u32 dln = 0u;
-    if (prefetch) rtn_load_group(a, gb, lane, qn, dln);
+    rtn_v4u qn[4], qn2[4];
+    rtn_u32 dln = 0u, dln2 = 0u;
+    if (prefetch) {
+      rtn_load_group(a, gb, lane, qn, dln);
+      if (gb + 1u < ge) rtn_load_group(a, gb + 1u, lane, qn2, dln2);
+    }
     for (rtn_u32 g = gb; g < ge; ++g) {
       rtn_u32 lo[16], dl;
       if (prefetch) {
@@ -642,7 +646,10 @@ __device__ __forceinline__ void rtn_run(const rtn_args& a) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) q[k] = qn[k];
         dl = dln;
-        if (g + 1u < ge) rtn_load_group(a, g + 1u, lane, qn, dln);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) qn[k] = qn2[k];
+        dln = dln2;
+        if (g + 2u < ge) rtn_load_group(a, g + 2u, lane, qn2, dln2);
         rtn_xpose(tile, lane, q, lo);
       } else if (slots64) {
         rtn_v4u q[4];
