@@ -633,11 +633,14 @@ __device__ __forceinline__ void rtn_run(const rtn_args& a) {
     // -0.4 % more, in-process A/B; with the split layout's dependent ext loads one group ahead
     // measured 5 % slower on cfg4 and is not used there)
     constexpr bool prefetch = MODE == RTN_S64;
+    // (the connection-stage instance keeps one group ahead: two would take it to 134 VGPRs, 3
+    // waves per SIMD)
+    constexpr bool ahead2 = prefetch && !CONN;
     rtn_v4u qn[4], qn2[4];
     rtn_u32 dln = 0u, dln2 = 0u;
     if (prefetch) {
       rtn_load_group(a, gb, lane, qn, dln);
-      if (gb + 1u < ge) rtn_load_group(a, gb + 1u, lane, qn2, dln2);
+      if (ahead2 && gb + 1u < ge) rtn_load_group(a, gb + 1u, lane, qn2, dln2);
     }
     for (rtn_u32 g = gb; g < ge; ++g) {
       rtn_u32 lo[16], dl;
@@ -646,10 +649,14 @@ __device__ __forceinline__ void rtn_run(const rtn_args& a) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) q[k] = qn[k];
         dl = dln;
+        if (ahead2) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) qn[k] = qn2[k];
-        dln = dln2;
-        if (g + 2u < ge) rtn_load_group(a, g + 2u, lane, qn2, dln2);
+          for (int k = 0; k < 4; ++k) qn[k] = qn2[k];
+          dln = dln2;
+          if (g + 2u < ge) rtn_load_group(a, g + 2u, lane, qn2, dln2);
+        } else if (g + 1u < ge) {
+          rtn_load_group(a, g + 1u, lane, qn, dln);
+        }
         rtn_xpose(tile, lane, q, lo);
       } else if (slots64) {
         rtn_v4u q[4];
