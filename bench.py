@@ -68,19 +68,12 @@ def gen_frames(cfg: str, n: int, start: int, threads: int = 8):
 
 def gen_rss_shard(cfg: str, n: int, rank: int, world: int, chunk: int = 1 << 21):
     """This rank's frames of the global stream [0, world * n) under Retina's symmetric RSS
-    (retina_amd/dist.py rss_hash / rss_rank): the frames whose RETA queue is this rank's. The
-    count per rank varies with the hash; every rank reads the whole stream to find its own."""
+    (retina_amd/dist.py rss_shard): each rank generates 1/world of the stream and the frames go
+    to the rank their RETA queue belongs to (an all-to-all at setup), so the count per rank
+    varies with the hash. Needs the process group for world > 1."""
     from retina_amd import dist as rdist
 
-    stride = CONFIGS[cfg][1]
-    slabs, dls = [], []
-    for s0 in range(0, world * n, chunk):
-        k = min(chunk, world * n - s0)
-        sl, dl = gen_frames(cfg, k, start=s0)
-        keep = rdist.rss_rank(rdist.rss_hash(sl, stride, dl), world) == rank
-        slabs.append(sl.reshape(k, stride)[keep].reshape(-1))
-        dls.append(dl[keep])
-    return np.concatenate(slabs), np.concatenate(dls)
+    return rdist.rss_shard(lambda k, s: gen_frames(cfg, k, start=s), CONFIGS[cfg][1], world * n, rank, world, chunk)
 
 
 def spec_for(cfg: str) -> str:
@@ -91,8 +84,14 @@ def spec_for(cfg: str) -> str:
 
 def _host_cpus() -> dict:
     """What this process may run on: the affinity mask, the machine's CPU count and the cgroup
-    CPU quota (cpu.max), which bounds the cores actually available when it is below the mask."""
+    CPU quota (cpu.max), which bounds the cores actually available when it is below the mask;
+    and the CPU model, so that baselines from different boxes can be told apart."""
     info = {"affinity": len(os.sched_getaffinity(0)), "nproc": os.cpu_count()}
+    try:
+        info["model"] = next(ln.split(":", 1)[1].strip() for ln in Path("/proc/cpuinfo").read_text().splitlines()
+                             if ln.startswith("model name"))
+    except Exception:
+        info["model"] = None
     try:
         q, per = Path("/sys/fs/cgroup/cpu.max").read_text().split()
         info["cgroup_quota_cpus"] = None if q == "max" else round(int(q) / int(per), 2)
@@ -328,6 +327,144 @@ def e2e_rate(ctx, slab: np.ndarray, dlen: np.ndarray, stride: int, dev, chunk: i
                     + (" and IPv6 addresses" if wide else "") + " straight into pinned host memory (zero-copy), "
                     "D2H of the bitmaps; PCIe-bound: h2d_only times the same host -> HBM copies alone; "
                     "mpps_with_d2h_copies copies the whole record buffers back instead"}
+
+
+def e2e_from_mbufs(ctx, slab: np.ndarray, dlen: np.ndarray, stride: int, dev, frames: int = 1 << 21,
+                   chunk: int = 1 << 19, nstreams: int = 4, threads: int | None = None) -> dict:
+    """End-to-end rate from DPDK-shaped mbufs (include/retina_stage.h): `frames` frames, each in
+    its own 2176-B buffer (128-B headroom) of a host mbuf pool, handed over in shuffled order as
+    an array of data pointers (buf_addr + data_off) + data_len, as rx_burst leaves them
+    (core/src/lcore/rx_core.rs:57-73). Two forms, each pipelined over `chunk`-frame sets on
+    `nstreams` streams, with the kernel writing its records straight into pinned host memory
+    and the bitmaps copied back (as e2e_rate):
+      host   -- rtn_stage_mbufs on pinned host threads into pinned staging buffers, H2D, kernel;
+      gpu    -- rtn_stage_gather: the GPU reads the mbufs from the registered pool, kernel."""
+    import torch
+
+    from retina_amd import pc
+
+    m = min(frames, len(dlen))
+    m -= m % 256
+    pool, ptrs = pc.mbuf_pool(slab[:m * stride], dlen[:m], stride, seed=17)
+    t0 = time.perf_counter()
+    mp = pc.MbufPool(pool, dev.index)  # hipHostRegister of the pool
+    t_reg = time.perf_counter() - t0
+    dl = np.ascontiguousarray(dlen[:m])
+    h_ptrs = torch.from_numpy(ptrs.view(np.int64)).pin_memory()
+    h_dl = torch.from_numpy(dl.view(np.int16)).pin_memory()
+    streams = [torch.cuda.Stream(dev) for _ in range(nstreams)]
+    rows_cap = pc.gather_ext_rows(chunk)
+    sets = []
+    for _ in range(nstreams):
+        out = ctx.alloc_outputs(chunk, addr6=True, counters=False)
+        h_l4 = torch.empty(out.l4.numel(), dtype=torch.uint8).pin_memory()
+        h_a6 = torch.empty(out.addr6.numel(), dtype=torch.uint8).pin_memory()
+        zc = dataclasses.replace(out, l4=pc.MappedHost(h_l4), addr6=pc.MappedHost(h_a6))
+        sets.append({
+            "head": torch.empty(chunk * 64, dtype=torch.uint8, device=dev),
+            "ext": torch.empty(rows_cap * 64, dtype=torch.uint8, device=dev),
+            "chunk": torch.empty(chunk // 256, dtype=torch.int32, device=dev),
+            "dl": torch.empty(chunk, dtype=torch.int16, device=dev),
+            "out": zc, "keep": (h_l4, h_a6),
+            "h_bm": torch.empty(out.pc_bitmap.numel() * 2, dtype=torch.uint8).pin_memory(),
+            # form (a): pinned host staging buffers of this set
+            "s_head": torch.empty(chunk * 64, dtype=torch.uint8).pin_memory(),
+            "s_ext": torch.empty(chunk * 64, dtype=torch.uint8).pin_memory(),
+            "s_chunk": torch.empty(chunk // 256, dtype=torch.int32).pin_memory(),
+            "s_dl": torch.empty(chunk, dtype=torch.int16).pin_memory(),
+            "done": None,
+        })
+    plan = [(s, min(chunk, m - s)) for s in range(0, m, chunk)]
+
+    def finish(k, st, b, nfr):
+        nb = b["out"].pc_bitmap.numel()
+        b["h_bm"][:nb].copy_(b["out"].pc_bitmap, non_blocking=True)
+        b["h_bm"][nb:].copy_(b["out"].fwd_bitmap, non_blocking=True)
+
+    def gpu_pass():
+        for k, (s, nfr) in enumerate(plan):
+            st, b = streams[k % nstreams], sets[k % nstreams]
+            with torch.cuda.stream(st):
+                mp.gather(h_ptrs[s:s + nfr], h_dl[s:s + nfr], nfr, b["head"], b["ext"], b["chunk"], b["dl"], stream=st)
+                ctx.run(b["head"], 64, b["dl"], nfr, b["out"], stream=st, ext=b["ext"], ext_chunk=b["chunk"])
+                finish(k, st, b, nfr)
+
+    def gather_only():
+        for k, (s, nfr) in enumerate(plan):
+            st, b = streams[k % nstreams], sets[k % nstreams]
+            mp.gather(h_ptrs[s:s + nfr], h_dl[s:s + nfr], nfr, b["head"], b["ext"], b["chunk"], b["dl"], stream=st)
+
+    cpus = sorted(os.sched_getaffinity(0))
+    q = _host_cpus()["cgroup_quota_cpus"]
+    if q:
+        cpus = cpus[:max(1, int(q))]
+    nthr = threads if threads is not None else max(1, len(cpus) - 2)  # leave the submitting thread a core
+    stager = pc.Stager(nthr, cpus[-nthr:] if len(cpus) >= nthr else None)
+    staged = {}
+
+    def stage(k, s, nfr, b):
+        rows, mx = stager.stage(ptrs[s:s + nfr], dl[s:s + nfr], b["s_head"], b["s_ext"], b["s_chunk"], b["s_dl"],
+                                n=nfr, cap=chunk, ext_cap=chunk)
+        staged[k] = (rows, mx)
+        return rows, mx
+
+    def host_pass():
+        for k, (s, nfr) in enumerate(plan):
+            st, b = streams[k % nstreams], sets[k % nstreams]
+            if b["done"] is not None:
+                b["done"].synchronize()  # the H2D copies of the set's previous chunk have left
+            rows, mx = stage(k, s, nfr, b)
+            with torch.cuda.stream(st):
+                b["head"][:nfr * 64].copy_(b["s_head"][:nfr * 64], non_blocking=True)
+                b["dl"][:nfr].copy_(b["s_dl"][:nfr], non_blocking=True)
+                if mx <= 64:  # every frame fits its 64-B slot: the 64-B-slot kernel (RTN_BATCH_DL_LE64)
+                    ctx.run(b["head"], 64, b["dl"], nfr, b["out"], stream=st, dl_le64=True)
+                else:
+                    if rows:
+                        b["ext"][:rows * 64].copy_(b["s_ext"][:rows * 64], non_blocking=True)
+                    b["chunk"][:(nfr + 255) // 256].copy_(b["s_chunk"][:(nfr + 255) // 256], non_blocking=True)
+                    ctx.run(b["head"], 64, b["dl"], nfr, b["out"], stream=st, ext=b["ext"][:max(rows, 1) * 64],
+                            ext_chunk=b["chunk"])
+                ev = torch.cuda.Event()
+                ev.record(st)
+                b["done"] = ev
+                finish(k, st, b, nfr)
+
+    def stage_only():
+        for k, (s, nfr) in enumerate(plan):
+            stage(k, s, nfr, sets[k % nstreams])
+
+    def timed(fn, reps=3):
+        fn()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize(dev)
+        return (time.perf_counter() - t0) / reps
+
+    res = {}
+    res["gpu"] = {"mpps": round(m / timed(gpu_pass) / 1e6, 1)}
+    assert mp.take_status() == 0, "rtn_stage_gather: a data pointer outside the pool"
+    dt = timed(gather_only)
+    res["gpu"]["gather_only_mpps"] = round(m / dt / 1e6, 1)
+    need = int(pc.ext_needed(slab[:m * stride].reshape(m, stride), dl).sum()) if stride > 64 else 0
+    pcie = m * (8 + 2 + 64) + need * 64
+    res["gpu"]["pcie_read_gbs"] = round(pcie / dt / 1e9, 2)
+    res["gpu"]["pcie_bytes_per_frame"] = round(pcie / m, 2)
+    res["host"] = {"mpps": round(m / timed(host_pass) / 1e6, 1), "threads": nthr}
+    res["host"]["stage_only_mpps"] = round(m / timed(stage_only) / 1e6, 1)
+    rows = sum(r for r, mx in staged.values() if mx > 64)  # ext rows copied (none when every frame fits 64 B)
+    res["host"]["h2d_bytes_per_frame"] = round((m * (64 + 2) + rows * 64) / m, 2)
+    win = max(res, key=lambda k: res[k]["mpps"])
+    del stager, mp
+    return {"frames": m, "chunk_frames": chunk, "streams": nstreams, "pool_bytes": int(pool.nbytes),
+            "pool_register_s": round(t_reg, 3), "ext_rows": need, **res, "winner": win,
+            "mpps": res[win]["mpps"],
+            "note": "mbuf-shaped buffers (2176 B, 128-B headroom, shuffled), data pointers + data_len as "
+                    "rx_burst leaves them; host = rtn_stage_mbufs threads into pinned buffers + H2D; "
+                    "gpu = rtn_stage_gather reading the hipHostRegister'd pool over PCIe; both then rtn_pc_run "
+                    "with records written into pinned host memory and the bitmaps copied back"}
 
 
 # Packet-level subscriptions that match at the protocol/session layer: their packets are
@@ -566,20 +703,28 @@ def main() -> None:
     counters = torch.cat([cnt_out.counters.view(torch.int32)[:3].to(torch.int64),
                           torch.tensor([n], dtype=torch.int64, device=dev)])
     stats = torch.tensor([wall, kern_ms, float(n)], dtype=torch.float64, device=dev)
+    per_rank = rdist.gather_rows([kern_ms, float(n), float(alg_bytes)], dev)  # [world, 3], for the report
     rdist.reduce_totals(counters, stats)  # sum / max over ranks (RCCL), outside the timed region
     wall, kern_ms, n_max = float(stats[0]), float(stats[1]), int(stats[2])
     counters = counters.cpu().tolist()
     total_frames = counters[3]
 
+    cpu = e2e = None
+    if rank == 0:
+        # the CPU baseline on the box's host cores in the same run, at every N (the other ranks
+        # wait at the barrier below, so their processes do not compete for the cores)
+        if not args.no_cpu:
+            cpu = cpu_baseline(cfg, slab, dlen, stride)
+        if not args.no_e2e and world == 1:
+            e2e = e2e_rate(ctx, slab, dlen, stride, dev, dl_le64=dl_le64, compact=compact or stride == 64)
+            e2e["from_mbufs"] = e2e_from_mbufs(ctx, slab, dlen, stride, dev)
+    rdist.host_barrier()
+
     if rank == 0:
         value = total_frames * args.steps / wall / 1e6  # every rank's frames over the slowest rank's time
         achieved = alg_bytes / (kern_ms / 1e3) / 1e9
-        cpu = None
-        if not args.no_cpu and world == 1:
-            cpu = cpu_baseline(cfg, slab, dlen, stride)
-        e2e = None
-        if not args.no_e2e and world == 1:
-            e2e = e2e_rate(ctx, slab, dlen, stride, dev, dl_le64=dl_le64, compact=compact or stride == 64)
+        ranks = [{"rank": r, "kernel_ms": round(float(k), 4), "frames": int(f),
+                  "frac": round(b / (k / 1e3) / 1e9 / HBM_PEAK_GBS, 4)} for r, (k, f, b) in enumerate(per_rank)]
         line = {
             "metric": METRIC,
             "value": round(value, 1),
@@ -602,6 +747,7 @@ def main() -> None:
                        "shard": {"mode": args.shard if world > 1 else "none", "frames_total": total_frames,
                                  "frames_max_rank": n_max,
                                  "imbalance": round(n_max * world / total_frames, 4)}},
+            "per_rank": ranks if world > 1 else None,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(cfg, n),
                          "alg_bytes_per_launch": alg_bytes, "kernel_ms": round(kern_ms, 4),

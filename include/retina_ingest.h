@@ -42,7 +42,8 @@ int32_t rtn_pcap_next_batch(rtn_pcap_t* p, uint8_t* slab, uint64_t stride, uint1
  * receives the first min(data_len, 64) bytes; a frame for which rtn_ext_needed() holds also gets
  * the next ext row (its bytes [64, 128)); ext_chunk[c] receives the first row of chunk c (RTN_CHUNK_FRAMES)
  * (ceil(cap / RTN_CHUNK_FRAMES) entries). *rows = rows written. The batch ends early, at a frame, when ext_cap
- * rows are used (allocate cap rows to never end early). */
+ * rows are used (allocate cap rows to never end early); if that frame is the batch's first, the call
+ * fails with RTN_ERANGE (*n = 0), so that *n == 0 with RTN_OK always means end of file. */
 int32_t rtn_pcap_next_batch_split(rtn_pcap_t* p, uint8_t* head, uint8_t* ext, uint32_t ext_cap, uint32_t* ext_chunk,
                                   uint16_t* data_len, uint32_t cap, uint32_t* n, uint32_t* rows);
 int32_t rtn_pcap_stats(const rtn_pcap_t* p, rtn_pcap_stats_t* st);

@@ -168,7 +168,10 @@ typedef struct rtn_pc_out {
   uint64_t* pc_bitmap;   /* [ceil(n/64)]  Actions.data contains PacketContinue               */
   uint64_t* fwd_bitmap;  /* [ceil(n/64)]  ... and L4Context::new succeeded (goes to conntrack) */
   rtn_l4ctx_t* l4;       /* [ceil(n/256)*256] (rtn_out_l4_bytes) at RTN_REC_INDEX; unused slots undefined */
-  uint8_t* addr6;        /* optional [ceil(n/256)*256][32]: src|dst of the IPv6 records   */
+  uint8_t* addr6;        /* optional [ceil(n/256)*256][32] (rtn_out_addr6_bytes): src|dst of the IPv6
+                          records; a chunk's last store is padded to whole 128-B lines, so it may
+                          write up to 3 entries past the chunk's last IPv6 record (inside the
+                          chunk's 256 entries)                                              */
   uint64_t* dlv_bitmap;  /* [ceil(n/64)] frames with >= 1 packet-level callback (if any)     */
   uint64_t* dlv_records; /* [ceil(n/256)*256][deliver_words]: statement mask; the frame is the
                           record's rank among its chunk's dlv_bitmap bits (as for l4)        */
@@ -255,8 +258,8 @@ int32_t rtn_pc_create(const char* spec, size_t len, int device, rtn_pc_t** out);
 int32_t rtn_pc_create_from_program(rtn_program_t* p, int device, rtn_pc_t** out);
 /* Launch on `stream` (a hipStream_t, NULL = default). Asynchronous. */
 int32_t rtn_pc_run(rtn_pc_t* pc, const rtn_batch_t* in, rtn_pc_out_t* out, void* stream);
-/* RTN_STATUS_* bits raised by runs without counters since the last call, then cleared.
- * Synchronizes the device. */
+/* RTN_STATUS_* bits raised by this context's runs without counters since the last call, then
+ * cleared. Waits for the context's last such run (not for the device or other streams). */
 int32_t rtn_pc_take_status(rtn_pc_t* pc, uint32_t* status);
 /* accepted_idx / n_accepted (the compaction form of SURVEY §8(b)) from any of the output
  * bitmaps (pc_bitmap, fwd_bitmap, dlv_bitmap), on `stream` after the run that wrote it:
@@ -269,6 +272,18 @@ int32_t rtn_pc_take_status(rtn_pc_t* pc, uint32_t* status);
  * Asynchronous; one scratch buffer per context, so calls on one context must not overlap. */
 int32_t rtn_pc_index(rtn_pc_t* pc, const uint64_t* bitmap, uint32_t n, uint32_t* idx, uint32_t* n_set,
                      uint32_t* chunk_base, void* stream);
+/* Launch shape of one of the context's kernel instances (diagnostics): layout 0 = monolithic
+ * slots, 1 = 64-byte slots, 2 = split, 3 = compact split; conn != 0 = the connection-stage
+ * instance. waves_per_simd is the runtime's occupancy for blocks of `threads` (registers and LDS);
+ * chunks_per_wave is what rtn_pc_run passes the compact split kernel (2 below 4 waves per SIMD). */
+typedef struct rtn_kernel_info {
+  uint32_t regs;            /* HIP_FUNC_ATTRIBUTE_NUM_REGS                 */
+  uint32_t lds_bytes;       /* static LDS per block                        */
+  uint32_t threads;         /* threads per block                           */
+  uint32_t waves_per_simd;  /* occupancy (0 if the runtime cannot say)     */
+  uint32_t chunks_per_wave;
+} rtn_kernel_info_t;
+int32_t rtn_pc_kernel_info(const rtn_pc_t* pc, uint32_t layout, uint32_t conn, rtn_kernel_info_t* info);
 /* Workgroups per launch (0 = default). */
 int32_t rtn_pc_set_grid(rtn_pc_t* pc, uint32_t blocks);
 int32_t rtn_pc_destroy(rtn_pc_t* pc);

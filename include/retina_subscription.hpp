@@ -185,18 +185,27 @@ class Burst {
 class Subscription {
  public:
   Subscription(const std::string& spec_toml, int device = 0) : device_(device) {
-    check(rtn_program_compile(spec_toml.data(), spec_toml.size(), &prog_));
-    check(rtn_program_info(prog_, &info_));
-    const uint32_t ns = info_.n_deliver_stmts;
-    std::vector<uint32_t> subs(ns ? ns : 1);
-    std::vector<uint8_t> pay(ns ? ns : 1);
-    check(rtn_program_deliver_table(prog_, subs.data(), pay.data(), ns ? ns : 1));
-    for (uint32_t k = 0; k < ns; ++k) {
-      std::string cb(rtn_program_deliver_callback(prog_, k, nullptr, 0), '\0');
-      rtn_program_deliver_callback(prog_, k, &cb[0], cb.size() + 1);
-      sites_.push_back({subs[k], cb, pay[k] != 0});
+    // a constructor that throws runs no destructor: release what was created before rethrowing
+    try {
+      check(rtn_program_compile(spec_toml.data(), spec_toml.size(), &prog_));
+      check(rtn_program_info(prog_, &info_));
+      const uint32_t ns = info_.n_deliver_stmts;
+      std::vector<uint32_t> subs(ns ? ns : 1);
+      std::vector<uint8_t> pay(ns ? ns : 1);
+      check(rtn_program_deliver_table(prog_, subs.data(), pay.data(), ns ? ns : 1));
+      for (uint32_t k = 0; k < ns; ++k) {
+        std::string cb(rtn_program_deliver_callback(prog_, k, nullptr, 0), '\0');
+        rtn_program_deliver_callback(prog_, k, &cb[0], cb.size() + 1);
+        sites_.push_back({subs[k], cb, pay[k] != 0});
+      }
+      check(rtn_pc_create_from_program(prog_, device, &pc_));
+    } catch (...) {
+      if (pc_) rtn_pc_destroy(pc_);
+      if (prog_) rtn_program_destroy(prog_);
+      pc_ = nullptr;
+      prog_ = nullptr;
+      throw;
     }
-    check(rtn_pc_create_from_program(prog_, device, &pc_));
   }
   Subscription(const Subscription&) = delete;
   Subscription& operator=(const Subscription&) = delete;

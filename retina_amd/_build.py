@@ -17,7 +17,7 @@ ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0]
 
 FILTERGEN_SRCS = ["ast.cpp", "parser.cpp", "filter.cpp", "ptree.cpp", "codegen.cpp", "hwfilter.cpp"]
 SO_NAME = "libretina_pc.so"
-RUNTIME_SRCS = ["runtime/rtn_runtime.cpp", "runtime/rtn_hw.cpp", "ingest/pcap_ingest.cpp"]
+RUNTIME_SRCS = ["runtime/rtn_runtime.cpp", "runtime/rtn_hw.cpp", "ingest/pcap_ingest.cpp", "ingest/mbuf_stage.cpp"]
 
 
 def _run(cmd: list[str], cwd: Path | None = None) -> None:
@@ -34,10 +34,10 @@ def _stale(target: Path, deps: list[Path]) -> bool:
     return any(d.stat().st_mtime > t for d in deps)
 
 
-def _gen_kernel_inc(name: str = "pc_kernel", var: str = "kPcKernelSrc") -> Path:
+def _gen_kernel_inc(name: str = "pc_kernel", var: str = "kPcKernelSrc", where: str = "runtime") -> Path:
     """Embed a kernel source as a C++ raw string (compiled by hiprtc at run time)."""
     src = CSRC / "kernels" / f"{name}.hip"
-    inc = CSRC / "runtime" / f"{name}_src.inc"
+    inc = CSRC / where / f"{name}_src.inc"
     text = src.read_text()
     delim = "RTNSRC"
     assert f"){delim}\"" not in text
@@ -51,14 +51,15 @@ def build_library(force: bool = False) -> Path:
     LIB.mkdir(exist_ok=True)
     inc = _gen_kernel_inc()
     inc_ct = _gen_kernel_inc("ct_kernel", "kCtKernelSrc")
+    inc_st = _gen_kernel_inc("stage_kernel", "kStageKernelSrc", "ingest")
     fg = [CSRC / "filtergen" / s for s in FILTERGEN_SRCS]
     rt = [CSRC / s for s in RUNTIME_SRCS]
     hdrs = (list((CSRC / "filtergen").glob("*.hpp")) + list((CSRC / "runtime").glob("*.hpp"))
-            + list((ROOT / "include").glob("*.h")) + [inc, inc_ct])
+            + list((ROOT / "include").glob("*.h")) + [inc, inc_ct, inc_st])
     so = LIB / SO_NAME
     if force or _stale(so, fg + rt + hdrs):
         cmd = [
-            "g++", "-std=c++17", "-O2", "-fPIC", "-shared", "-Wall", "-Wextra", "-Wno-unused-parameter",
+            "g++", "-std=c++17", "-O2", "-fPIC", "-shared", "-pthread", "-Wall", "-Wextra", "-Wno-unused-parameter",
             "-D__HIP_PLATFORM_AMD__", f"-I{ROOT / 'include'}", f"-I{ROCM / 'include'}",
             *map(str, fg), *map(str, rt), "-o", str(so),
             f"-L{ROCM / 'lib'}", f"-Wl,-rpath,{ROCM / 'lib'}", "-lamdhip64", "-lhiprtc",
@@ -89,6 +90,12 @@ def build_kernel_check() -> Path:
     """Ahead-of-time hipcc compile of the kernel template with the config-2 filter spliced in
     (the same translation unit hiprtc builds at run time) to catch template breakage at build."""
     so = LIB / SO_NAME
+    # the program-independent gather kernel (rtn_stage_gather), hiprtc-compiled at pool registration
+    st_src = CSRC / "kernels" / "stage_kernel.hip"
+    st_out = LIB / "stage_kernel.hsaco"
+    if _stale(st_out, [st_src]):
+        _run([str(ROCM / "bin" / "hipcc"), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "--genco",
+              str(st_src), "-o", str(st_out)])
     out = LIB / "pc_kernel_cfg2.hsaco"
     src = LIB / "pc_kernel_cfg2.hip"
     tpl = CSRC / "kernels" / "pc_kernel.hip"

@@ -229,6 +229,11 @@ int32_t rtn_pcap_next_batch_split(rtn_pcap_t* p, uint8_t* head, uint8_t* ext, ui
     if (need && r == ext_cap) {  // no row left: end the batch before this frame
       p->off = at;
       p->st.frames--;
+      if (k == 0) {  // an empty batch always means end of file: say why this one is empty
+        *n = 0;
+        *rows = 0;
+        return rtn::set_error(RTN_ERANGE, "no ext row free for the next frame (ext_cap too small)");
+      }
       break;
     }
     if (k % RTN_CHUNK_FRAMES == 0) ext_chunk[k / RTN_CHUNK_FRAMES] = r;

@@ -68,7 +68,9 @@ struct rtn_args {
   rtn_u64* pc_bm;             // [ceil(n/64)]  PacketContinue bit
   rtn_u64* fwd_bm;            // [ceil(n/64)]  PacketContinue && L4Context::new Ok
   rtn_l4rec* recs;            // [ceil(n/256)*256], dense per chunk
-  unsigned char* addr6;       // [ceil(n/64)*64][32] (src, dst) raw bytes, IPv6 records only
+  unsigned char* addr6;       // [ceil(n/256)*256][32] (rtn_out_addr6_bytes) (src, dst) raw bytes, IPv6
+                              // records only; rtn_flush6 pads a chunk's last store to whole lines,
+                              // up to 3 entries past its last record (inside the chunk's 256)
   rtn_u64* dlv_bm;            // [ceil(n/64)]  any packet-level delivery
   rtn_u64* dlv_recs;          // [ceil(n/256)*256][RTN_DELIVER_WORDS] statement masks, ranked by dlv_bm per chunk
   rtn_u32* counters;          // [0] pc, [1] fwd, [2] dlv, [3] status, [4..5] bytes, [6..7] ignored bytes,

@@ -203,6 +203,14 @@ int32_t compile_code_object(const std::string& src, std::shared_ptr<std::vector<
   return RTN_OK;
 }
 
+}  // namespace
+
+int32_t rtn::compile_hip(const std::string& src, std::shared_ptr<std::vector<uint8_t>>& out) {
+  return compile_code_object(src, out);
+}
+
+namespace {
+
 // kernel argument block; must match struct rtn_args in pc_kernel.hip
 struct KArgs {
   const unsigned char* slab;
@@ -263,6 +271,17 @@ struct IdxArgs {
 };
 constexpr uint32_t RTN_IDX_WORDS = 4096;  // bitmap words per block, must match pc_kernel.hip
 
+// Waves per SIMD a kernel reaches in blocks of `threads` (the runtime's occupancy calculator:
+// registers and LDS); 0 if it cannot say.
+uint32_t waves_per_simd(hipFunction_t f, uint32_t threads) {
+  int blocks = 0;
+  if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, f, (int)threads, 0) != hipSuccess || blocks <= 0) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return (uint32_t)blocks * (threads / 64u) / 4u;  // 4 SIMDs per CU
+}
+
 }  // namespace
 
 struct rtn_program {
@@ -291,7 +310,11 @@ struct rtn_pc {
   // used when the caller passes no counters: word RTN_CNT_STATUS accumulates the status bits of
   // such runs until rtn_pc_take_status reads and clears them (the other words are never read)
   uint32_t* scratch_counters = nullptr;
+  hipEvent_t last_nc = nullptr;  // recorded after each run without counters (rtn_pc_take_status)
+  hipStream_t own = nullptr;     // private non-blocking stream of rtn_pc_take_status
   ~rtn_pc() {
+    if (last_nc) (void)hipEventDestroy(last_nc);
+    if (own) (void)hipStreamDestroy(own);
     if (scratch_counters) (void)hipFree(scratch_counters);
     if (idx_block_sum) (void)hipFree(idx_block_sum);
     if (module) (void)hipModuleUnload(module);
@@ -505,17 +528,14 @@ int32_t rtn_pc_create_from_program(rtn_program_t* p, int device, rtn_pc_t** out)
       if (e != hipSuccess) return fail(RTN_EDEVICE, std::string("hipModuleGetFunction: ") + hipGetErrorString(e));
     }
   }
-  // two consecutive chunks per wave when the compact split kernel's VGPRs hold it below 4 waves
-  // per SIMD (its LDS allows 4): see the chunk loop in pc_kernel.hip
-  auto cpw_for = [](hipFunction_t f, const char* name) {
-    int vgprs = 0;
-    uint32_t cpw = 1;
-    if (hipFuncGetAttribute(&vgprs, HIP_FUNC_ATTRIBUTE_NUM_REGS, f) == hipSuccess && vgprs > 0) {
-      const int regs = (vgprs + 7) / 8 * 8;  // allocation granule
-      cpw = 512 / regs < 4 ? 2u : 1u;
-    }
+  // two consecutive chunks per wave when the compact split kernel's occupancy (registers, VGPRs
+  // and AGPRs, and LDS, as the runtime computes it) is below 4 waves per SIMD: see the chunk loop
+  // in pc_kernel.hip
+  auto cpw_for = [pc = pc.get()](hipFunction_t f, const char* name) {
+    const uint32_t waves = waves_per_simd(f, pc->threads);
+    const uint32_t cpw = waves != 0 && waves < 4 ? 2u : 1u;
 #ifdef RTN_EXPERIMENTS
-    if (getenv("RTN_DEBUG")) fprintf(stderr, "%s: %d VGPRs, %u chunks per wave\n", name, vgprs, cpw);
+    if (getenv("RTN_DEBUG")) fprintf(stderr, "%s: %u waves per SIMD, %u chunks per wave\n", name, waves, cpw);
 #else
     (void)name;
 #endif
@@ -538,6 +558,9 @@ int32_t rtn_pc_create_from_program(rtn_program_t* p, int device, rtn_pc_t** out)
   if (e != hipSuccess) return fail(RTN_EDEVICE, std::string("hipMalloc: ") + hipGetErrorString(e));
   e = hipMemset(pc->scratch_counters, 0, RTN_COUNTERS_BYTES);
   if (e != hipSuccess) return fail(RTN_EDEVICE, std::string("hipMemset: ") + hipGetErrorString(e));
+  e = hipEventCreateWithFlags(&pc->last_nc, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&pc->own, hipStreamNonBlocking);
+  if (e != hipSuccess) return fail(RTN_EDEVICE, std::string("rtn_pc_create: ") + hipGetErrorString(e));
 #ifdef RTN_EXPERIMENTS
   if (const char* g = getenv("RTN_GRID")) pc->blocks = (uint32_t)strtoul(g, nullptr, 10);
   if (const char* b = getenv("RTN_BLOCK")) pc->threads = (uint32_t)strtoul(b, nullptr, 10);
@@ -557,6 +580,23 @@ int32_t rtn_pc_create(const char* spec, size_t len, int device, rtn_pc_t** out) 
     return rc;
   }
   (*out)->owned = p;
+  return RTN_OK;
+}
+
+int32_t rtn_pc_kernel_info(const rtn_pc_t* pc, uint32_t layout, uint32_t conn, rtn_kernel_info_t* info) {
+  if (!pc || !info) return fail(RTN_EINVAL, "null argument");
+  if (layout > 3) return fail(RTN_EINVAL, "layout must be 0..3");
+  const hipFunction_t plain[4] = {pc->fn, pc->fn_s64, pc->fn_split, pc->fn_splitc};
+  const hipFunction_t f = conn ? pc->fn_conn[layout] : plain[layout];
+  int regs = 0, lds = 0;
+  hipError_t e = hipFuncGetAttribute(&regs, HIP_FUNC_ATTRIBUTE_NUM_REGS, f);
+  if (e == hipSuccess) e = hipFuncGetAttribute(&lds, HIP_FUNC_ATTRIBUTE_SHARED_SIZE_BYTES, f);
+  if (e != hipSuccess) return fail(RTN_EDEVICE, std::string("hipFuncGetAttribute: ") + hipGetErrorString(e));
+  info->regs = (uint32_t)regs;
+  info->lds_bytes = (uint32_t)lds;
+  info->threads = pc->threads;
+  info->waves_per_simd = waves_per_simd(f, pc->threads);
+  info->chunks_per_wave = layout == 3 ? (conn ? pc->splitc_cpw_conn : pc->splitc_cpw) : 1u;
   return RTN_OK;
 }
 
@@ -635,6 +675,11 @@ int32_t rtn_pc_run(rtn_pc_t* pc, const rtn_batch_t* in, rtn_pc_out_t* out, void*
   hipFunction_t fn = out->conn ? pc->fn_conn[layout] : plain[layout];
   e = hipModuleLaunchKernel(fn, blocks, 1, 1, threads, 1, 1, 0, s, params, nullptr);
   if (e != hipSuccess) return fail(RTN_EDEVICE, std::string("hipModuleLaunchKernel: ") + hipGetErrorString(e));
+  // a run without counters reports its status bits in the context's word: remember where it ends
+  if (!out->counters) {
+    e = hipEventRecord(pc->last_nc, s);
+    if (e != hipSuccess) return fail(RTN_EDEVICE, std::string("hipEventRecord: ") + hipGetErrorString(e));
+  }
   return RTN_OK;
 }
 
@@ -700,11 +745,14 @@ int32_t rtn_pc_index(rtn_pc_t* pc, const uint64_t* bitmap, uint32_t n, uint32_t*
 
 int32_t rtn_pc_take_status(rtn_pc_t* pc, uint32_t* status) {
   if (!pc || !status) return fail(RTN_EINVAL, "null argument");
+  // waits for this context's last run without counters only (not the device): the status word is
+  // read and cleared on the context's own stream
   hipError_t e = hipSetDevice(pc->device);
-  if (e == hipSuccess) e = hipDeviceSynchronize();
-  if (e == hipSuccess) e = hipMemcpy(status, pc->scratch_counters + RTN_CNT_STATUS, 4, hipMemcpyDeviceToHost);
-  if (e == hipSuccess) e = hipMemset(pc->scratch_counters + RTN_CNT_STATUS, 0, 4);
-  if (e == hipSuccess) e = hipDeviceSynchronize();
+  if (e == hipSuccess) e = hipEventSynchronize(pc->last_nc);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(status, pc->scratch_counters + RTN_CNT_STATUS, 4, hipMemcpyDeviceToHost, pc->own);
+  if (e == hipSuccess) e = hipMemsetAsync(pc->scratch_counters + RTN_CNT_STATUS, 0, 4, pc->own);
+  if (e == hipSuccess) e = hipStreamSynchronize(pc->own);
   return e == hipSuccess ? RTN_OK : fail(RTN_EDEVICE, std::string("rtn_pc_take_status: ") + hipGetErrorString(e));
 }
 

@@ -1,10 +1,13 @@
 """Multi-GPU sharding for the packet stage.
 
-Packets are independent at this stage, so ranks never exchange packet data: rank r filters its
-own contiguous shard of the frame stream on its own GPU (weak scaling). The only collective is
-the reduction of per-rank totals and timings, once, outside the timed region — SURVEY §8e's
-`allreduce(sum)` of {packets, accepted, forwarded, delivered} plus a max of the per-rank times.
-The same functions run over RCCL ("nccl") on GPUs and over gloo in the CPU tests.
+Packets are independent at this stage, so ranks never exchange packet data on the data path:
+rank r filters its own shard of the frame stream on its own GPU (weak scaling). The only
+collectives are the reduction of per-rank totals and timings, once, outside the timed region --
+SURVEY §8e's `allreduce(sum)` of {packets, accepted, forwarded, delivered} plus a max of the
+per-rank times -- a gather of the per-rank kernel times for the report, and, for RSS shards only,
+an all-to-all of the generated frames at setup (each rank generates 1/world of the stream and
+sends every frame to the rank its RSS queue belongs to). The same functions run over RCCL
+("nccl") on GPUs and over gloo in the CPU tests.
 """
 from __future__ import annotations
 
@@ -120,3 +123,105 @@ def reduce_totals(totals, times):
 def aggregate_mpps(frames_per_rank: int, world: int, steps: int, max_wall_s: float) -> float:
     """Whole-job throughput: every rank's frames over the slowest rank's time."""
     return frames_per_rank * world * steps / max_wall_s / 1e6
+
+
+def gather_rows(row, device=None) -> np.ndarray:
+    """Every rank's float64 row (same length on all ranks) as a [world, k] array, on every rank;
+    the row itself when no process group is up. Outside any timed region."""
+    import torch
+    import torch.distributed as dist
+
+    r = np.asarray(row, np.float64)
+    if not (dist.is_available() and dist.is_initialized()):
+        return r[None, :]
+    on_dev = dist.get_backend() == "nccl"
+    t = torch.from_numpy(r.copy())
+    if on_dev:
+        t = t.to(device)
+    out = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return np.stack([o.cpu().numpy() for o in out])
+
+
+_HOST_GROUP = None
+
+
+def _host_group():
+    """A gloo group over all ranks (host memory, blocking waits), created once."""
+    import torch.distributed as dist
+
+    global _HOST_GROUP
+    if _HOST_GROUP is None:
+        _HOST_GROUP = dist.new_group(backend="gloo") if dist.get_backend() != "gloo" else dist.group.WORLD
+    return _HOST_GROUP
+
+
+def host_barrier() -> None:
+    """A barrier whose waiting ranks block in a socket read (gloo) instead of polling the GPU
+    stream: rank 0 times the CPU baseline on the host cores while the others wait here."""
+    import torch.distributed as dist
+
+    if dist.is_available() and dist.is_initialized():
+        dist.barrier(group=_host_group())
+
+
+def exchange(parts: list) -> list:
+    """All-to-all of byte arrays: parts[d] (uint8) goes to rank d; returns, by source rank, the
+    arrays every rank sent this one. Setup only (RSS shards): it runs over a gloo group on host
+    memory whatever the main backend is, so the same code path runs here and on the GPU node."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size()
+    g = _host_group()
+    sizes = torch.tensor([int(p.size) for p in parts], dtype=torch.int64)
+    got = torch.empty(world, dtype=torch.int64)
+    dist.all_to_all_single(got, sizes, group=g)
+    send = torch.from_numpy(np.concatenate([np.ascontiguousarray(p, np.uint8).reshape(-1) for p in parts]))
+    recv = torch.empty(int(got.sum()), dtype=torch.uint8)
+    dist.all_to_all_single(recv, send, got.tolist(), sizes.tolist(), group=g)
+    r = recv.numpy()
+    offs = np.concatenate([[0], np.cumsum(got.numpy())])
+    return [r[offs[k]:offs[k + 1]] for k in range(world)]
+
+
+def rss_shard(gen, stride: int, total: int, rank: int, world: int, chunk: int = 1 << 21):
+    """This rank's frames of the global stream [0, total) under Retina's symmetric RSS (rss_hash,
+    rss_rank), in stream order. `gen(k, start)` returns (slab, dlen) of frames [start, start + k).
+    Rank r generates only the stream's chunks r, r + world, ... (1/world of the stream), hashes
+    them, and sends every frame to its queue's rank (exchange); chunks are then reassembled in
+    stream order from the per-chunk counts, so the result equals filtering the whole stream."""
+    nch = (total + chunk - 1) // chunk
+    counts = np.zeros((world, nch), np.int64)  # frames of my chunks per destination
+    slabs = [[] for _ in range(world)]
+    dls = [[] for _ in range(world)]
+    for c in range(rank, nch, world):
+        s0 = c * chunk
+        k = min(chunk, total - s0)
+        sl, dl = gen(k, s0)
+        q = rss_rank(rss_hash(sl, stride, dl), world)
+        rows = sl.reshape(k, stride)
+        for d in range(world):
+            sel = q == d
+            counts[d, c] = int(sel.sum())
+            slabs[d].append(rows[sel].reshape(-1))
+            dls[d].append(dl[sel])
+    cat = lambda xs, dt: np.concatenate(xs) if xs else np.zeros(0, dt)  # noqa: E731
+    if world == 1:
+        return cat(slabs[0], np.uint8), cat(dls[0], np.uint16)
+    rc = [x.view(np.int64) for x in exchange([counts[d].view(np.uint8) for d in range(world)])]
+    rs = exchange([cat(slabs[d], np.uint8) for d in range(world)])
+    rd = [x.view(np.uint16) for x in exchange([cat(dls[d], np.uint16).view(np.uint8) for d in range(world)])]
+    n = int(sum(int(x.sum()) for x in rc))
+    slab = np.empty(n * stride, np.uint8)
+    dlen = np.empty(n, np.uint16)
+    off = [0] * world
+    at = 0
+    for c in range(nch):  # chunk c came from rank c % world
+        src = c % world
+        k = int(rc[src][c])
+        slab[at * stride:(at + k) * stride] = rs[src][off[src] * stride:(off[src] + k) * stride]
+        dlen[at:at + k] = rd[src][off[src]:off[src] + k]
+        off[src] += k
+        at += k
+    return slab, dlen

@@ -53,6 +53,11 @@ class _PcapStats(C.Structure):
     _fields_ = [("frames", C.c_uint64), ("skipped_mtu", C.c_uint64), ("packed", C.c_uint64), ("bytes", C.c_uint64)]
 
 
+class _StageSlab(C.Structure):
+    _fields_ = [("head", C.c_void_p), ("ext", C.c_void_p), ("ext_chunk", C.c_void_p), ("data_len", C.c_void_p),
+                ("cap", C.c_uint32), ("ext_cap", C.c_uint32)]
+
+
 class _Info(C.Structure):
     _fields_ = [("n_subscriptions", C.c_uint32), ("n_deliver_stmts", C.c_uint32),
                 ("deliver_words", C.c_uint32), ("tree_size", C.c_uint32), ("n_conn_stmts", C.c_uint32),
@@ -95,6 +100,7 @@ EXPORTS = {
     "rtn_pc_create_from_program": (C.c_int32, [C.c_void_p, C.c_int, C.POINTER(C.c_void_p)]),
     "rtn_pc_run": (C.c_int32, [C.c_void_p, C.POINTER(_Batch), C.POINTER(_Out), C.c_void_p]),
     "rtn_pc_set_grid": (C.c_int32, [C.c_void_p, C.c_uint32]),
+    "rtn_pc_kernel_info": (C.c_int32, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p]),
     "rtn_pc_take_status": (C.c_int32, [C.c_void_p, C.POINTER(C.c_uint32)]),
     "rtn_pc_index": (C.c_int32, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "rtn_pc_destroy": (C.c_int32, [C.c_void_p]),
@@ -134,6 +140,17 @@ EXPORTS = {
     "rtn_pcap_stats": (C.c_int32, [C.c_void_p, C.POINTER(_PcapStats)]),
     "rtn_pcap_rewind": (C.c_int32, [C.c_void_p]),
     "rtn_pcap_close": (None, [C.c_void_p]),
+    # include/retina_stage.h
+    "rtn_stager_create": (C.c_int32, [C.c_uint32, C.c_void_p, C.POINTER(C.c_void_p)]),
+    "rtn_stager_destroy": (None, [C.c_void_p]),
+    "rtn_stage_mbufs": (C.c_int32, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p,
+                                    C.POINTER(C.c_uint32), C.POINTER(C.c_uint16)]),
+    "rtn_mbuf_pool_register": (C.c_int32, [C.c_void_p, C.c_size_t, C.c_int, C.POINTER(C.c_void_p)]),
+    "rtn_mbuf_pool_destroy": (C.c_int32, [C.c_void_p]),
+    "rtn_stage_gather_ext_rows": (C.c_uint32, [C.c_uint32]),
+    "rtn_stage_gather": (C.c_int32, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p,
+                                     C.c_void_p]),
+    "rtn_mbuf_pool_take_status": (C.c_int32, [C.c_void_p, C.POINTER(C.c_uint32)]),
 }
 
 
@@ -439,6 +456,13 @@ class PacketContinue:
         if getattr(self, "_h", None) and self._h.value and _lib is not None:
             _lib.rtn_pc_destroy(self._h)
             self._h = C.c_void_p()
+
+    def kernel_info(self, layout: int, conn: bool = False) -> dict:
+        """rtn_pc_kernel_info: registers, LDS, occupancy and chunks per wave of one kernel instance
+        (layout 0 monolithic, 1 64-byte slots, 2 split, 3 compact split)."""
+        w = (C.c_uint32 * 5)()
+        _check(lib().rtn_pc_kernel_info(self._h, layout, 1 if conn else 0, C.byref(w)))
+        return dict(zip(("regs", "lds_bytes", "threads", "waves_per_simd", "chunks_per_wave"), list(w)))
 
     def set_grid(self, blocks: int) -> None:
         _check(lib().rtn_pc_set_grid(self._h, blocks))
@@ -831,3 +855,109 @@ def hw_patterns(filter_str: str, validate=None) -> str:
     buf = C.create_string_buffer(need + 1)
     L.rtn_hw_patterns(filter_str.encode(), cb, None, buf, need + 1)
     return buf.value.decode()
+
+
+# ----------------------------------------------------------------------------------------------
+# Staging DPDK RX bursts (include/retina_stage.h): mbuf data pointers -> the compact split layout.
+
+STATUS_BAD_MBUF = 8  # RTN_STATUS_BAD_MBUF
+
+
+def _addr(x) -> int:
+    """Address of a numpy array or a torch tensor (or a MappedHost)."""
+    if isinstance(x, np.ndarray):
+        return x.ctypes.data
+    return x.data_ptr()
+
+
+class Stager:
+    """rtn_stage_mbufs: host worker threads gather mbufs (by data pointer = buf_addr + data_off)
+    into the compact split layout in host memory: head slots, data_len, exactly compact ext rows
+    and ext_chunk (the layout rtn_pc_run reads with RTN_BATCH_EXT_COMPACT)."""
+
+    def __init__(self, threads: int = 0, cpus=None):
+        h = C.c_void_p()
+        arr = (C.c_int32 * len(cpus))(*cpus) if cpus else None
+        _check(lib().rtn_stager_create(threads, arr, C.byref(h)))
+        self._h = h
+        self.threads = threads
+
+    def __del__(self):
+        if getattr(self, "_h", None) and self._h.value and _lib is not None:
+            _lib.rtn_stager_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def stage(self, ptrs: np.ndarray, data_len: np.ndarray, head, ext, ext_chunk, dlen_out, n: int | None = None,
+              cap: int | None = None, ext_cap: int | None = None) -> tuple[int, int]:
+        """ptrs: uint64[n] data pointers; data_len: uint16[n]. head / ext / ext_chunk / dlen_out:
+        host buffers (numpy arrays or pinned torch tensors) sized for cap frames / ext_cap rows.
+        Returns (rows, dl_max)."""
+        n = len(ptrs) if n is None else n
+        cap = (head.nbytes if isinstance(head, np.ndarray) else head.numel()) // 64 if cap is None else cap
+        if ext_cap is None:
+            ext_cap = (ext.nbytes if isinstance(ext, np.ndarray) else ext.numel()) // 64
+        slab = _StageSlab(_addr(head), _addr(ext), _addr(ext_chunk), _addr(dlen_out), cap, ext_cap)
+        rows, mx = C.c_uint32(), C.c_uint16()
+        _check(lib().rtn_stage_mbufs(self._h, C.c_void_p(_addr(ptrs)), C.c_void_p(_addr(data_len)), n,
+                                     C.byref(slab), C.byref(rows), C.byref(mx)))
+        return rows.value, mx.value
+
+
+def gather_ext_rows(n: int) -> int:
+    """Ext rows rtn_stage_gather writes for n frames (256 per chunk)."""
+    return int(lib().rtn_stage_gather_ext_rows(n))
+
+
+class MbufPool:
+    """rtn_mbuf_pool_register: a host memory range holding mbuf buffers, mapped for the GPU
+    (hipHostRegister), from which rtn_stage_gather pulls frames over PCIe. `host` is a numpy
+    array or a torch CPU tensor that stays alive while the pool exists."""
+
+    def __init__(self, host, device: int = 0):
+        self.host = host
+        nbytes = host.nbytes if isinstance(host, np.ndarray) else host.numel() * host.element_size()
+        self.base = _addr(host)
+        self.nbytes = nbytes
+        h = C.c_void_p()
+        _check(lib().rtn_mbuf_pool_register(C.c_void_p(self.base), nbytes, device, C.byref(h)))
+        self._h = h
+        self.device = device
+
+    def __del__(self):
+        if getattr(self, "_h", None) and self._h.value and _lib is not None:
+            _lib.rtn_mbuf_pool_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def gather(self, ptrs, data_len, n: int, head, ext, ext_chunk, dlen_out, status=None, stream=None) -> None:
+        """rtn_stage_gather on `stream`: ptrs (uint64) and data_len (uint16) device-readable
+        (device or pinned host tensors); outputs device tensors. Asynchronous."""
+        import torch
+
+        slab = _StageSlab(_addr(head), _addr(ext), _addr(ext_chunk), _addr(dlen_out), head.numel() // 64,
+                          ext.numel() // 64)
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        _check(lib().rtn_stage_gather(self._h, C.c_void_p(_addr(ptrs)), C.c_void_p(_addr(data_len)), n,
+                                      C.byref(slab), C.c_void_p(_addr(status) if status is not None else 0),
+                                      C.c_void_p(s.cuda_stream)))
+
+    def take_status(self) -> int:
+        st = C.c_uint32()
+        _check(lib().rtn_mbuf_pool_take_status(self._h, C.byref(st)))
+        return int(st.value)
+
+
+def mbuf_pool(slab: np.ndarray, dlen: np.ndarray, stride: int, buf: int = 2176, headroom: int = 128,
+              seed: int = 1, alloc=None):
+    """A DPDK-shaped mbuf pool holding the frames of a slot slab: one `buf`-byte buffer per frame
+    (RTE_MBUF_DEFAULT_BUF_SIZE 2176, headroom 128, core/src/memory/mempool.rs:26-29), in a
+    shuffled order as a mempool hands them out after some churn. Buffer b receives its frame's
+    slot bytes at headroom. Returns (pool uint8 array, data pointers uint64[n]).
+    `alloc(nbytes)` may supply the (e.g. pinned) backing array."""
+    n = len(dlen)
+    raw = alloc(n * buf + 4096) if alloc is not None else np.zeros(n * buf + 4096, np.uint8)
+    off = (-_addr(raw)) % 4096  # page-aligned pool (hipHostRegister pins whole pages), 128-B buffers
+    pool = raw[off:off + n * buf]
+    perm = np.random.default_rng(seed).permutation(n)
+    pool.reshape(n, buf)[perm, headroom:headroom + stride] = slab.reshape(n, stride)
+    ptrs = (_addr(pool) + perm.astype(np.uint64) * buf + headroom).astype(np.uint64)
+    return pool, ptrs

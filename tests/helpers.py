@@ -66,6 +66,15 @@ def gpu_run(spec: str, slab: np.ndarray, stride: int, dlen: np.ndarray, device: 
     dl_t = torch.from_numpy(np.ascontiguousarray(dlen, np.uint16).view(np.int16)).to(dev)
     out = ctx.run(slab_t, stride, dl_t, n, out=ctx.alloc_outputs(max(n, 1), conn=conn), ext=ext_t, ext_chunk=chunk_t)
     torch.cuda.synchronize()
+    res = canonical(prog, out, dlen, conn=conn)
+    assert res["counters"][3] == 0 or stride == 64, res["counters"]
+    return res
+
+
+def canonical(prog, out, dlen: np.ndarray, conn: bool = False) -> dict:
+    """A finished run's outputs (pc.PCOutputs with counters) in the canonical per-frame form of
+    oracle_run, after checking the byte / protocol counters of the same launch."""
+    n = len(dlen)
     d = out.decode()
     cnt = out.counters_host()
     # TOTAL_BYTE / IGNORED_BY_PACKET_FILTER_BYTE (rx_core.rs:129-141) from the same launch
@@ -80,7 +89,6 @@ def gpu_run(spec: str, slab: np.ndarray, stride: int, dlen: np.ndarray, device: 
     tcp = l4["proto"] == 6
     assert (st["TCP_PKT"], st["UDP_PKT"]) == (int(tcp.sum()), int((~tcp).sum())), st
     assert (st["TCP_BYTE"], st["UDP_BYTE"]) == (int(dl64[fidx[tcp]].sum()), int(dl64[fidx[~tcp]].sum())), st
-    assert cnt[3] == 0 or stride == 64, cnt
     rec = np.zeros(len(l4), REC)
     for f in ("ver", "proto", "flags", "sport", "dport", "offset", "length"):
         rec[f] = l4[f]

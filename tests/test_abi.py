@@ -269,3 +269,30 @@ def test_deliver_callbacks_name_each_statement():
         cbs = [s.callback for s in filterlang.load_spec(SETS[fset])]
         assert prog.deliver_callbacks() == [cbs[int(s)] for s in subs]
         assert pc.lib().rtn_program_deliver_callback(prog._h, prog.info["n_deliver_stmts"], None, 0) == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fset", ["cfg2", "cfg3", "cfg4"])
+def test_chunks_per_wave_follow_occupancy(gpu, fset):
+    """rtn_pc_run gives the compact split kernel 2 chunks per wave exactly when the runtime's
+    occupancy (registers incl. AGPRs, and LDS) holds it below 4 waves per SIMD, and
+    that occupancy agrees with the code object's own register and LDS counts."""
+    import sys
+
+    sys.path.insert(0, str(Path(__file__).resolve().parent.parent / "tools"))
+    import kernel_resources
+
+    prog = pc.Program.from_spec(SETS[fset])
+    meta = {r["kernel"]: r for r in kernel_resources.report(prog.code_object())}
+    ctx = pc.PacketContinue(prog, 0)
+    names = ["rtn_pc_kernel", "rtn_pc_kernel_s64", "rtn_pc_kernel_split", "rtn_pc_kernel_splitc"]
+    for layout, name in enumerate(names):
+        for conn in (False, True):
+            i = ctx.kernel_info(layout, conn)
+            m = meta[name + ("_conn" if conn else "")]
+            reg_bound = 512 // max(8, -(-m["vgpr"] // 8) * 8)
+            lds_bound = (160 * 1024 // max(m["lds"], 1)) * (i["threads"] // 64) // 4
+            assert i["lds_bytes"] == m["lds"], (name, conn, i, m)
+            assert 1 <= i["waves_per_simd"] <= min(8, reg_bound, lds_bound), (name, conn, i, m)
+            want = 2 if layout == 3 and i["waves_per_simd"] < 4 else 1
+            assert i["chunks_per_wave"] == want, (name, conn, i)

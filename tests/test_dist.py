@@ -122,18 +122,53 @@ def test_toeplitz_known_answers_and_symmetry():
     assert set(ranks.tolist()) == set(range(8))
 
 
-def test_rss_shards_partition_the_stream():
-    """bench.py --shard rss: the ranks' frames partition the global stream (every frame on exactly
-    one rank, frame order kept) and the per-rank counts are near even."""
+def _rss_rank_main(rank: int, world: int, port: int, n: int, chunk: int, q) -> None:
+    import sys
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parent.parent
+    sys.path[:0] = [str(root), str(root / "tests")]
+    import torch.distributed as dist
+
     import bench
     from retina_amd import dist as rdist
 
-    n, world = 1 << 14, 4
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        s, d = bench.gen_rss_shard("cfg3", n, rank, world, chunk=chunk)
+        rdist.host_barrier()
+        q.put((rank, s, d))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,chunk", [(4, 1 << 12), (3, 5000), (2, 1 << 21)])
+def test_rss_shards_partition_the_stream(world, chunk):
+    """bench.py --shard rss: each rank generates 1/world of the stream (chunks r, r + world, ...)
+    and sends every frame to the rank of its RSS queue (an all-to-all over gloo); the ranks' frames
+    then partition the global stream (every frame on exactly one rank, stream order kept), exactly
+    as filtering the whole stream per rank would, and the per-rank counts are near even."""
+    import multiprocessing as mp
+
+    import bench
+    from retina_amd import dist as rdist
+
+    n = 1 << 14
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rss_rank_main, args=(r, world, port, n, chunk, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    parts = dict((r, (s, d)) for r, s, d in (q.get(timeout=240) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
     full, fd = bench.gen_frames("cfg3", world * n, 0)
-    parts = [bench.gen_rss_shard("cfg3", n, r, world) for r in range(world)]
-    assert sum(len(d) for _, d in parts) == world * n
+    assert sum(len(d) for _, d in parts.values()) == world * n
     rk = rdist.rss_rank(rdist.rss_hash(full, 128, fd), world)
-    for r, (s, d) in enumerate(parts):
+    for r, (s, d) in parts.items():
         assert np.array_equal(d, fd[rk == r])
         assert np.array_equal(s.reshape(-1, 128), full.reshape(-1, 128)[rk == r])
         assert abs(len(d) - n) < n * 0.1

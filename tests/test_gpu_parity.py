@@ -159,9 +159,11 @@ def test_full_size_cfg2_properties(gpu):
     assert np.array_equal(l4["seq_no"][sel], ora["rec"]["seq"])
 
 
+@pytest.mark.parametrize("layout", ["compact", "split"])
 @pytest.mark.parametrize("cfg,n", [("cfg3", 1 << 24), ("cfg4", 1 << 23)])
-def test_full_size_split_properties(cfg, n, gpu):
-    """BASELINE configs 3 and 4 at full size in the split layout the bench uses: the counters
+def test_full_size_split_properties(cfg, n, layout, gpu):
+    """BASELINE configs 3 and 4 at full size in the compact split layout bench.py times (and in
+    the plain split layout): the counters
     equal the bitmaps' popcounts, the forwarded set is inside the accepted set, every record is a
     well-formed L4Context (protocol, version, offset, UDP fields), the TCP/UDP byte counters equal
     the data_len sums of the decoded records, and two 64K-frame windows (the start of the second
@@ -172,11 +174,16 @@ def test_full_size_split_properties(cfg, n, gpu):
 
     slab, dlen = bench.gen_frames(cfg, n, 0)
     spec = SETS[cfg]
-    head, ext = pc.split_slab(slab, 128)
     ctx = pc.PacketContinue(pc.Program.from_spec(spec), 0)
     dev = torch.device("cuda", 0)
+    chunk_t = None
+    if layout == "compact":  # bench.py's layout (RTN_BATCH_EXT_COMPACT)
+        head, ext, chunk = pc.split_slab(slab, 128, dlen, compact=True)
+        chunk_t = torch.from_numpy(chunk.view(np.int32)).to(dev)
+    else:
+        head, ext = pc.split_slab(slab, 128)
     out = ctx.run(torch.from_numpy(head).to(dev), 64, torch.from_numpy(dlen.view(np.int16)).to(dev), n,
-                  ext=torch.from_numpy(ext).to(dev))
+                  ext=torch.from_numpy(ext).to(dev), ext_chunk=chunk_t)
     del head, ext
     torch.cuda.synchronize()
     d = out.decode()

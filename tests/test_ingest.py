@@ -169,3 +169,27 @@ def test_split_batches_match_the_slot_layout(tmp_path, ext_cap):
     for j, i in enumerate(np.nonzero(need)[0]):
         k = min(int(dlen[i]), 128) - 64
         assert exts[j, :k].tobytes() == full[i, 64:64 + k].tobytes()
+
+
+def test_split_batch_without_rows_is_not_eof(tmp_path):
+    """A compact split batch that cannot take its first frame (no ext row free) fails with
+    RTN_ERANGE instead of returning an empty batch, which callers read as end of file."""
+    import corpus as C
+
+    long = [(f + bytes(600), len(f) + 600) for f in C.base_frames()]
+    s0, d0 = pc.pack_frames([f for f, _ in long], 128)
+    nd = pc.ext_needed(s0.reshape(-1, 128), d0)
+    long = [fr for fr, k in zip(long, nd) if k]  # frames that need an ext row
+    assert len(long) > 2
+    p = tmp_path / "d.pcap"
+    _write_pcap(p, long)
+    slab, dlen = pc.PcapReader(p).read_all(stride=128)
+    r = pc.PcapReader(p)
+    cap = 16
+    head, ext = np.zeros(cap * 64, np.uint8), np.zeros(64, np.uint8)
+    ch, d = np.zeros(1, np.uint32), np.zeros(cap, np.uint16)
+    with pytest.raises(pc.RetinaError) as e:
+        r.next_batch_split(head, ext[:0], ch, d)  # ext_cap 0
+    assert e.value.code == -34
+    k, rows = r.next_batch_split(head, ext, ch, d)  # one row: the same first frame, then stop
+    assert k >= 1 and rows == 1 and d[0] == dlen[0]
