@@ -260,12 +260,13 @@ def e2e_rate(ctx, slab: np.ndarray, dlen: np.ndarray, stride: int, dev, chunk: i
                      torch.empty(chunk // pc.CHUNK_FRAMES + 1, dtype=torch.int32, device=dev),
                      ctx.alloc_outputs(chunk, addr6=wide, counters=False)))
     h_out = [torch.empty(bufs[0][4].l4.numel(), dtype=torch.uint8).pin_memory() for _ in range(nstreams)]
+    h_t4 = [torch.empty(bufs[0][4].tcp4.numel(), dtype=torch.uint8).pin_memory() for _ in range(nstreams)]
     h_bm = [torch.empty(bufs[0][4].pc_bitmap.numel() * 2, dtype=torch.uint8).pin_memory() for _ in range(nstreams)]
     h_a6 = [torch.empty(bufs[0][4].addr6.numel(), dtype=torch.uint8).pin_memory() for _ in range(nstreams)] if wide else None
 
     # zero-copy outputs: the kernel writes records (and IPv6 addresses) straight into pinned host
     # memory over PCIe, so only what was produced crosses the link (pc.MappedHost)
-    zc_outs = [dataclasses.replace(bufs[k][4], l4=pc.MappedHost(h_out[k]),
+    zc_outs = [dataclasses.replace(bufs[k][4], l4=pc.MappedHost(h_out[k]), tcp4=pc.MappedHost(h_t4[k]),
                                    addr6=pc.MappedHost(h_a6[k]) if wide else None) for k in range(nstreams)]
 
     def one_pass(zero_copy: bool = True):
@@ -286,6 +287,7 @@ def e2e_rate(ctx, slab: np.ndarray, dlen: np.ndarray, stride: int, dev, chunk: i
                     ctx.run(d_slab, run_stride, d_dlen, m, out, stream=st, dl_le64=dl_le64)
                 if not zero_copy:
                     h_out[k % nstreams].copy_(out.l4, non_blocking=True)
+                    h_t4[k % nstreams].copy_(out.tcp4, non_blocking=True)
                     if wide:
                         h_a6[k % nstreams].copy_(out.addr6, non_blocking=True)
                 nb = out.pc_bitmap.numel()
@@ -359,13 +361,14 @@ def e2e_from_mbufs(ctx, slab: np.ndarray, dlen: np.ndarray, stride: int, dev, fr
         out = ctx.alloc_outputs(chunk, addr6=True, counters=False)
         h_l4 = torch.empty(out.l4.numel(), dtype=torch.uint8).pin_memory()
         h_a6 = torch.empty(out.addr6.numel(), dtype=torch.uint8).pin_memory()
-        zc = dataclasses.replace(out, l4=pc.MappedHost(h_l4), addr6=pc.MappedHost(h_a6))
+        h_t4 = torch.empty(out.tcp4.numel(), dtype=torch.uint8).pin_memory()
+        zc = dataclasses.replace(out, l4=pc.MappedHost(h_l4), addr6=pc.MappedHost(h_a6), tcp4=pc.MappedHost(h_t4))
         sets.append({
             "head": torch.empty(chunk * 64, dtype=torch.uint8, device=dev),
             "ext": torch.empty(rows_cap * 64, dtype=torch.uint8, device=dev),
             "chunk": torch.empty(chunk // 256, dtype=torch.int32, device=dev),
             "dl": torch.empty(chunk, dtype=torch.int16, device=dev),
-            "out": zc, "keep": (h_l4, h_a6),
+            "out": zc, "keep": (h_l4, h_a6, h_t4),
             "h_bm": torch.empty(out.pc_bitmap.numel() * 2, dtype=torch.uint8).pin_memory(),
             # form (a): pinned host staging buffers of this set
             "s_head": torch.empty(chunk * 64, dtype=torch.uint8).pin_memory(),
@@ -703,7 +706,9 @@ def main() -> None:
     counters = torch.cat([cnt_out.counters.view(torch.int32)[:3].to(torch.int64),
                           torch.tensor([n], dtype=torch.int64, device=dev)])
     stats = torch.tensor([wall, kern_ms, float(n)], dtype=torch.float64, device=dev)
-    per_rank = rdist.gather_rows([kern_ms, float(n), float(alg_bytes)], dev)  # [world, 3], for the report
+    # [world, 4], for the report: every rank reaches this line only after its own oracle windows
+    # passed (verify_sample raises on any difference)
+    per_rank = rdist.gather_rows([kern_ms, float(n), float(alg_bytes), float(len(verified["windows"]))], dev)
     rdist.reduce_totals(counters, stats)  # sum / max over ranks (RCCL), outside the timed region
     wall, kern_ms, n_max = float(stats[0]), float(stats[1]), int(stats[2])
     counters = counters.cpu().tolist()
@@ -724,7 +729,8 @@ def main() -> None:
         value = total_frames * args.steps / wall / 1e6  # every rank's frames over the slowest rank's time
         achieved = alg_bytes / (kern_ms / 1e3) / 1e9
         ranks = [{"rank": r, "kernel_ms": round(float(k), 4), "frames": int(f),
-                  "frac": round(b / (k / 1e3) / 1e9 / HBM_PEAK_GBS, 4)} for r, (k, f, b) in enumerate(per_rank)]
+                  "frac": round(b / (k / 1e3) / 1e9 / HBM_PEAK_GBS, 4), "verified_windows": int(v)}
+                 for r, (k, f, b, v) in enumerate(per_rank)]
         line = {
             "metric": METRIC,
             "value": round(value, 1),

@@ -122,8 +122,8 @@ void walk(const HostSet& h, bool with_ct, Totals& t, FILE* dump) {
             p = dst;
             for (int j = 16; j < 32; ++j) p += sprintf(p, "%02x", a[j]);
           } else {
-            sprintf(src, "%08x", r.src_ip4);
-            sprintf(dst, "%08x", r.dst_ip4);
+            sprintf(src, "%08x", r.w0);  // an IPv4 record's addresses
+            sprintf(dst, "%08x", r.w1);
           }
           fprintf(dump, "%llu %u %s %u %s %u %u %u\n", (unsigned long long)(h.first_frame + i), RTN_L4_PROTO(r.meta),
                   src, r.ports & 0xffffu, dst, r.ports >> 16, status, slot);

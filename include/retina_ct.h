@@ -66,7 +66,7 @@ typedef struct rtn_ct_stats {
 int32_t rtn_ct_create(int device, uint32_t capacity_log2, uint32_t max_connections, rtn_ct_t** out);
 int32_t rtn_ct_destroy(rtn_ct_t* ct);
 /* One batch (n frames, the same batch rtn_pc_run processed into `pc`): two launches on `stream`.
- * out: device array of rtn_out_l4_bytes(n) / 24 * 8 bytes (rtn_out_ct_bytes). */
+ * out: device array of rtn_out_ct_bytes(n) bytes, indexed like the records. */
 int32_t rtn_ct_process(rtn_ct_t* ct, const rtn_pc_out_t* pc, uint32_t n, rtn_ct_entry_t* out, void* stream);
 /* Remove connections (device array of slot handles); their slots become tombstones. */
 int32_t rtn_ct_remove(rtn_ct_t* ct, const uint32_t* slots, uint32_t n, void* stream);

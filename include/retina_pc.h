@@ -48,15 +48,18 @@ extern "C" {
 typedef struct rtn_program rtn_program_t; /* compiled subscription set (host only)        */
 typedef struct rtn_pc rtn_pc_t;           /* program loaded on one device, ready to run  */
 
-/* Compacted L4Context of a forwarded packet (PacketContinue && L4Context::new Ok), 24 bytes:
- * every field of conntrack/pdu.rs:66-84. The frame it belongs to is implied by the record's
- * position (see rtn_pc_out_t). */
+/* Compacted L4Context of a forwarded packet (PacketContinue && L4Context::new Ok), 16 bytes.
+ * Together with its side streams it holds every field of conntrack/pdu.rs:66-84, and no field
+ * that is always zero for the record's kind:
+ *   IPv4 TCP: w0 = src, w1 = dst (u32::from(Ipv4Addr), host order); seq_no | ack_no << 32 in tcp4
+ *   IPv4 UDP: w0 = src, w1 = dst                                       (seq_no = ack_no = 0)
+ *   IPv6 TCP: w0 = seq_no, w1 = ack_no; src | dst in addr6
+ *   IPv6 UDP: w0 = w1 = 0;              src | dst in addr6             (seq_no = ack_no = 0)
+ * The frame a record belongs to is implied by its position (see rtn_pc_out_t). */
 typedef struct rtn_l4ctx {
-  uint32_t src_ip4; /* u32::from(Ipv4Addr) (host order); 0 for IPv6, see addr6 array     */
-  uint32_t dst_ip4;
+  uint32_t w0;
+  uint32_t w1;
   uint32_t ports;   /* src_port | dst_port << 16                                         */
-  uint32_t seq_no;  /* TCP only (0 for UDP)                                              */
-  uint32_t ack_no;  /* TCP only                                                          */
   uint32_t meta;    /* RTN_L4_* accessors below: offset, proto, ip version, flags, length */
 } rtn_l4ctx_t;
 
@@ -67,6 +70,9 @@ typedef struct rtn_l4ctx {
 #define RTN_L4_IPV6(m) (((m) >> 7) & 1u)                           /* src/dst are IPv6 (addr6)   */
 #define RTN_L4_FLAGS(m) (((m) >> 8) & 0xFFu)                       /* L4Context.flags (TCP)      */
 #define RTN_L4_LENGTH(m) ((m) >> 16)                               /* L4Context.length           */
+/* seq_no | ack_no << 32 of an IPv4 TCP record, in rtn_pc_out_t.tcp4 */
+#define RTN_TCP4_SEQ(t) ((uint32_t)(t))
+#define RTN_TCP4_ACK(t) ((uint32_t)((t) >> 32))
 
 /* Connection stage of a forwarded frame (8 bytes, indexed like its rtn_l4ctx_t):
  *   hash  = rtn_conn_hash of the canonical ConnId: MurmurHash3-x86-32 block + finaliser steps,
@@ -157,13 +163,14 @@ static inline int rtn_ext_needed(const uint8_t* head, uint16_t data_len) {
  * partly-forwarded batch stay dense).
  * The j-th forwarded IPv6 frame of chunk c (records with RTN_L4_IPV6) has its addresses at
  * addr6[c * RTN_CHUNK_FRAMES + j]; dlv_records are ranked by dlv_bitmap the same way (dense per
- * chunk). Bitmaps hold bit i % 64 of word i / 64. */
+ * chunk). The j-th IPv4 TCP record of chunk c (neither RTN_L4_IPV6 nor UDP) has its seq/ack at
+ * tcp4[RTN_REC_INDEX(n, c, j)]. Bitmaps hold bit i % 64 of word i / 64. */
 #define RTN_CHUNK_FRAMES 256u
 #define RTN_REC_BLOCK 64u
 #define RTN_REC_INDEX(n, chunk, k)                                                             \
   (((uint64_t)((k) / RTN_REC_BLOCK) * (((uint64_t)(n) + RTN_CHUNK_FRAMES - 1u) / RTN_CHUNK_FRAMES) + \
     (uint64_t)(chunk)) * RTN_REC_BLOCK + (uint64_t)((k) % RTN_REC_BLOCK))
-/* l4, addr6 and conn must be 16-byte aligned (RTN_EINVAL otherwise). */
+/* l4, addr6, conn and tcp4 must be 16-byte aligned (RTN_EINVAL otherwise). */
 typedef struct rtn_pc_out {
   uint64_t* pc_bitmap;   /* [ceil(n/64)]  Actions.data contains PacketContinue               */
   uint64_t* fwd_bitmap;  /* [ceil(n/64)]  ... and L4Context::new succeeded (goes to conntrack) */
@@ -180,6 +187,8 @@ typedef struct rtn_pc_out {
   rtn_conn_t* conn;      /* optional [ceil(n/256)*256]: connection stage, indexed like l4       */
   uint64_t* conn_dlv;    /* [ceil(n/256)*256][conn_words] first-packet statement masks; required
                           with conn when the program has first-packet statements           */
+  uint64_t* tcp4;        /* optional [ceil(n/256)*256] (rtn_out_tcp4_bytes): seq_no | ack_no << 32
+                          of the IPv4 TCP records (NULL: not written)                       */
 } rtn_pc_out_t;
 
 /* The counters block (u32 word offsets; the byte sums are u64 over two words). The stats names
@@ -295,6 +304,7 @@ size_t rtn_out_addr6_bytes(uint32_t n);
 size_t rtn_out_dlv_bytes(uint32_t n, uint32_t deliver_words);
 size_t rtn_out_conn_bytes(uint32_t n);
 size_t rtn_out_conn_dlv_bytes(uint32_t n, uint32_t conn_words);
+size_t rtn_out_tcp4_bytes(uint32_t n);
 
 #ifdef __cplusplus
 }

@@ -12,6 +12,7 @@
 #include "retina_stage.h"
 
 #include <hip/hip_runtime.h>
+#include <immintrin.h>
 #include <pthread.h>
 #include <sched.h>
 
@@ -89,6 +90,28 @@ struct rtn_stager {
 
 namespace {
 
+// 64 bytes into a head slot or ext row: plain copy, or (experiments build, RTN_STAGE_NT) streaming
+// stores that skip the read-for-ownership of the destination line.
+#ifdef RTN_EXPERIMENTS
+const bool kStageNt = getenv("RTN_STAGE_NT") != nullptr;
+#else
+constexpr bool kStageNt = false;
+#endif
+inline void copy64(uint8_t* dst, const uint8_t* src) {
+  if (kStageNt) {
+    const __m128i* s = reinterpret_cast<const __m128i*>(src);
+    __m128i* d = reinterpret_cast<__m128i*>(dst);
+    const __m128i a = _mm_loadu_si128(s), b = _mm_loadu_si128(s + 1), c = _mm_loadu_si128(s + 2),
+                  e = _mm_loadu_si128(s + 3);
+    _mm_stream_si128(d, a);
+    _mm_stream_si128(d + 1, b);
+    _mm_stream_si128(d + 2, c);
+    _mm_stream_si128(d + 3, e);
+  } else {
+    memcpy(dst, src, 64);
+  }
+}
+
 // Pass 1 over frames [f0, f1) (whole chunks): head slots, data_len, need bits, rows per chunk.
 void stage_heads(const uint8_t* const* data, const uint16_t* dl, uint32_t f0, uint32_t f1,
                  const rtn_stage_slab_t& s, uint64_t* need, uint32_t* chunk_rows, uint16_t& dl_max) {
@@ -99,7 +122,7 @@ void stage_heads(const uint8_t* const* data, const uint16_t* dl, uint32_t f0, ui
     if (i + kPrefetch < f1) __builtin_prefetch(data[i + kPrefetch]);
     const uint8_t* src = data[i];
     uint8_t* h = s.head + (uint64_t)i * 64u;
-    memcpy(h, src, 64);
+    copy64(h, src);
     const uint16_t d = dl[i];
     s.data_len[i] = d;
     mx = d > mx ? d : mx;
@@ -129,7 +152,7 @@ void stage_ext(const uint8_t* const* data, uint32_t f0, uint32_t f1, const rtn_s
       }
       while (b) {
         const uint32_t i = w * 64u + (uint32_t)__builtin_ctzll(b);
-        memcpy(s.ext + row * 64u, data[i] + 64, 64);
+        copy64(s.ext + row * 64u, data[i] + 64);
         ++row;
         b &= b - 1u;
       }
@@ -198,6 +221,7 @@ int32_t rtn_stage_mbufs(rtn_stager_t* st, const uint8_t* const* data, const uint
     };
     st->run_all();
   }
+  if (kStageNt) _mm_sfence();
   uint64_t r = 0;
   for (uint32_t c = 0; c < nch; ++c) {
     s.ext_chunk[c] = (uint32_t)r;
@@ -218,6 +242,7 @@ int32_t rtn_stage_mbufs(rtn_stager_t* st, const uint8_t* const* data, const uint
       st->run_all();
     }
   }
+  if (kStageNt) _mm_sfence();
   *rows = (uint32_t)r;
   return RTN_OK;
 }

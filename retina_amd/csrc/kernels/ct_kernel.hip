@@ -20,8 +20,8 @@
 //                  (CAS on the tag), then lower the slot's `first` to their frame index.
 //   rtn_ct_lookup  every forwarded frame finds its key (tags, then the whole key, so a 64-bit
 //                  fingerprint collision is reported instead of aliasing) and gets its status.
-// A block walks one 256-frame chunk, a wave one group: lane = frame, records ranked by the fwd
-// bitmap exactly as rtn_pc_run wrote them.
+// A wave walks one 256-frame chunk record by record (lane = record, see below), records ranked by
+// the fwd bitmap exactly as rtn_pc_run wrote them.
 #ifndef __HIPCC_RTC__
 #include <hip/hip_runtime.h>
 #endif
@@ -32,6 +32,7 @@ typedef unsigned long long rtn_u64;
 #define RTN_CT_CHUNK 256u   // RTN_CHUNK_FRAMES
 #define RTN_CT_GROUPS (RTN_CT_CHUNK / 64u)
 #define RTN_CT_MAXPROBE 256u
+#define RTN_CT_NO_SLOT_K 0xffffffffu  // RTN_CT_NO_SLOT
 #define RTN_CT_EMPTY 0ull
 #define RTN_CT_REMOVED 1ull
 
@@ -46,7 +47,7 @@ typedef unsigned long long rtn_u64;
 
 struct rtn_ct_args {
   const rtn_u64* fwd_bm;
-  const rtn_u32* recs;        // rtn_l4ctx_t, 6 words each
+  const rtn_u32* recs;        // rtn_l4ctx_t, 4 words each (w0, w1, ports, meta)
   const rtn_u32* addr6;       // 8 words per IPv6 record
   const rtn_u64* conn;        // rtn_conn_t
   rtn_u64* out;               // rtn_ct_entry_t (slot | status << 32), indexed like recs
@@ -85,11 +86,11 @@ __device__ __forceinline__ rtn_u32 rtn_ct_fmix(rtn_u32 h) {
   return h ^ (h >> 16);
 }
 
-// Canonical key of a record (its 6 words, its rtn_conn_t, its IPv6 addresses or null) + its
-// 64-bit fingerprint.
-__device__ __forceinline__ void rtn_ct_make_key(const rtn_ct_args& a, const rtn_u32 (&rec)[6], rtn_u64 c,
+// Canonical key of a record (its 4 words, its rtn_conn_t, its IPv6 addresses or null) + its
+// 64-bit fingerprint. An IPv4 record's words 0 and 1 are its addresses.
+__device__ __forceinline__ void rtn_ct_make_key(const rtn_ct_args& a, const rtn_u32 (&rec)[4], rtn_u64 c,
                                                 const rtn_u32* a6, rtn_ct_key& k) {
-  const rtn_u32 meta = rec[5];
+  const rtn_u32 meta = rec[3];
   k.h = (rtn_u32)c;
   k.info = (rtn_u32)(c >> 32);
   k.v6 = (meta >> 7) & 1u;
@@ -133,6 +134,13 @@ __device__ __forceinline__ void rtn_ct_make_key(const rtn_ct_args& a, const rtn_
   if (k.fp < 2ull) k.fp += 2ull;
 }
 
+// LDS visibility between lanes of one wave
+__device__ __forceinline__ void rtn_ct_wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 __device__ __forceinline__ bool rtn_ct_occupied(const rtn_u32* occ, rtn_u32 slot) {
   return (occ[slot >> 5] >> (slot & 31u)) & 1u;
 }
@@ -141,233 +149,286 @@ __device__ __forceinline__ rtn_u64* rtn_ct_tag(const rtn_ct_args& a, rtn_u32 slo
   return reinterpret_cast<rtn_u64*>(a.table + (rtn_u64)slot * 16u);
 }
 
-#ifndef RTN_CT_GPW
-#define RTN_CT_GPW 2u  // 64-frame groups per wave (cfg2 steady pass: 1 -> 0.62, 2 -> 0.52, 4 -> 0.62, 8 -> 1.13 ms)
-#endif
-// Chunks per block. The insert pass's block takes 2 (4 waves), so its admission costs one
-// reservation atomic per 512 frames (one per 256-frame chunk: cfg2 first pass 1.37 -> 1.98 ms);
-// the lookup's takes 1 (2 waves: steady pass 0.512 ms with 2 chunks per block, 0.484 with 1).
-#define RTN_CT_INSERT_CPB 2u
-#define RTN_CT_LOOKUP_CPB 1u
-#define RTN_CT_WPC (RTN_CT_GROUPS / RTN_CT_GPW)  // waves per chunk
+// Record-major walk. One wave per 256-frame chunk (RTN_CT_CPB chunks per block); lane l takes the
+// chunk's records l, l + 64, ... (a pass per 64 records), so that a wave's loads do not wait for
+// the forwarded bitmap: the first pass's rtn_conn_t loads go out with the bitmap words (record
+// slot RTN_REC_INDEX(n, c, k) needs only k), and every lane of a pass holds a record. A record's
+// frame index is recovered from the chunk's bitmap words (the k-th set bit). The records that
+// need the table (openers in the insert pass, frames whose start slot is occupied in the lookup)
+// are then compacted into a per-wave LDS list and handled 64 at a time, so the dependent table
+// reads run on full waves.
+#define RTN_CT_CPB 4u     // chunks (waves) per block
+#define RTN_CT_PASSES 4u  // RTN_CT_CHUNK / 64
 
-// One block per chunk; each wave takes RTN_CT_GPW groups and issues all of their loads
-// before using any (the walk is latency-bound: a wave per group left too few loads in flight).
-// The record rank comes from the chunk's RTN_CT_GROUPS bitmap words; the IPv6 rank needs the IPv6 counts of
-// the earlier groups, exchanged through LDS. fn(lane has a record, record index, frame index,
-// record words, rtn_conn_t, IPv6 addresses or null) runs for every lane of every wave (lanes
-// without a record pass has == false) so that waves can cooperate inside it; it builds the key
-// only if it needs it.
-struct rtn_ct_frames {  // this lane's frame in each of the wave's RTN_CT_GPW groups
-  bool has[RTN_CT_GPW];
-  rtn_u64 r[RTN_CT_GPW], cv[RTN_CT_GPW];
-  rtn_u32 frame[RTN_CT_GPW];
-  rtn_u32 rec[RTN_CT_GPW][6];
-  const rtn_u32* a6[RTN_CT_GPW];
+// position of the r-th set bit of x (r < popcount(x))
+__device__ __forceinline__ rtn_u32 rtn_ct_select(rtn_u64 x, rtn_u32 r) {
+  rtn_u32 pos = 0u;
+#pragma unroll
+  for (rtn_u32 w = 32u; w >= 1u; w >>= 1) {
+    const rtn_u64 low = x & ((1ull << w) - 1ull);
+    const rtn_u32 c = (rtn_u32)__popcll(low);
+    const bool up = r >= c;
+    r = up ? r - c : r;
+    x = up ? x >> w : low;
+    pos += up ? w : 0u;
+  }
+  return pos;
+}
+
+struct rtn_ct_chunk {
+  rtn_u32 c;          // chunk index (wave-uniform)
+  rtn_u64 nch;        // chunks in the batch
+  rtn_u64 w[4];       // the chunk's forwarded-bitmap words (wave-uniform)
+  rtn_u32 p0, p01, p012, total;  // prefix popcounts
 };
 
-template <rtn_u32 CPB>
-__device__ __forceinline__ void rtn_ct_load(const rtn_ct_args& a, rtn_ct_frames& f) {
-  constexpr rtn_u32 G = RTN_CT_GPW;
-  __shared__ rtn_u32 v6cnt_all[CPB][RTN_CT_GROUPS];
-  const rtn_u32 lane = threadIdx.x & 63u;
-  const rtn_u32 wb = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const rtn_u32 w = wb % RTN_CT_WPC;                   // wave within its chunk
-  const rtn_u32 c = blockIdx.x * CPB + wb / RTN_CT_WPC;
-  rtn_u32* v6cnt = v6cnt_all[wb / RTN_CT_WPC];
-  const rtn_u64 lane_lt = lane ? (~0ull >> (64u - lane)) : 0ull;
+// All-ones/zero lane mask hidden from the optimiser, so that a select chain stays v_cndmask /
+// v_bfi instead of being folded into a dynamically indexed private array (scratch).
+__device__ __forceinline__ rtn_u32 rtn_ct_mask(bool b) {
+  rtn_u32 m = b ? 0xffffffffu : 0u;
+  asm("" : "+v"(m));
+  return m;
+}
+__device__ __forceinline__ rtn_u32 rtn_ct_sel(rtn_u32 m, rtn_u32 x, rtn_u32 y) { return (x & m) | (y & ~m); }
+
+// frame index of the chunk's k-th forwarded frame
+__device__ __forceinline__ rtn_u32 rtn_ct_frame(const rtn_ct_chunk& ch, rtn_u32 k) {
+  const rtn_u32 ma = rtn_ct_mask(k < ch.p0), mb = rtn_ct_mask(k < ch.p01), md = rtn_ct_mask(k < ch.p012);
+  const rtn_u32 lo = rtn_ct_sel(ma, (rtn_u32)ch.w[0], rtn_ct_sel(mb, (rtn_u32)ch.w[1], rtn_ct_sel(md, (rtn_u32)ch.w[2], (rtn_u32)ch.w[3])));
+  const rtn_u32 hi = rtn_ct_sel(ma, (rtn_u32)(ch.w[0] >> 32),
+                                rtn_ct_sel(mb, (rtn_u32)(ch.w[1] >> 32), rtn_ct_sel(md, (rtn_u32)(ch.w[2] >> 32), (rtn_u32)(ch.w[3] >> 32))));
+  const rtn_u32 before = rtn_ct_sel(ma, 0u, rtn_ct_sel(mb, ch.p0, rtn_ct_sel(md, ch.p01, ch.p012)));
+  const rtn_u32 base = rtn_ct_sel(ma, 0u, rtn_ct_sel(mb, 64u, rtn_ct_sel(md, 128u, 192u)));
+  return ch.c * RTN_CT_CHUNK + base + rtn_ct_select((rtn_u64)lo | ((rtn_u64)hi << 32), k - before);
+}
+
+__device__ __forceinline__ rtn_u64 rtn_ct_rslot(const rtn_ct_chunk& ch, rtn_u32 k) {  // RTN_REC_INDEX
+  return ((rtn_u64)(k >> 6) * ch.nch + ch.c) * 64u + (k & 63u);
+}
+
+__device__ __forceinline__ rtn_u64 rtn_ct_rl64(rtn_u64 v, int l) {
+  return (rtn_u64)__builtin_amdgcn_readlane((rtn_u32)v, l) | ((rtn_u64)__builtin_amdgcn_readlane((rtn_u32)(v >> 32), l) << 32);
+}
+
+// The chunk's bitmap words and the rtn_conn_t of its records: cv[j] / has[j] for record
+// k = 64 j + lane; pass 0's load is issued with the bitmap words. v6r[j]: the record's rank
+// among the chunk's IPv6 records (its addr6 row is c * 256 + v6r).
+__device__ __forceinline__ void rtn_ct_begin(const rtn_ct_args& a, rtn_u32 c, rtn_u32 lane, rtn_ct_chunk& ch,
+                                             rtn_u64 (&cv)[RTN_CT_PASSES], bool (&has)[RTN_CT_PASSES],
+                                             rtn_u32 (&v6r)[RTN_CT_PASSES]) {
   const rtn_u32 nw = (a.n + 63u) / 64u;
-  const rtn_u64 nch = ((rtn_u64)a.n + RTN_CT_CHUNK - 1u) / RTN_CT_CHUNK;
-  // the chunk's bitmap words: lane j < RTN_CT_GROUPS holds word j; pre[j] = records before group j
-  const rtn_u32 gj = c * RTN_CT_GROUPS + (lane & (RTN_CT_GROUPS - 1u));
-  const rtn_u64 word = gj < nw ? a.fwd_bm[gj] : 0ull;
-  const rtn_u32 pop = (rtn_u32)__popcll(word);
-  // (q = w * G + u is not a compile-time index: accumulate per group instead of indexing an array)
-  rtn_u32 pre[G];
+  ch.c = c;
+  ch.nch = ((rtn_u64)a.n + RTN_CT_CHUNK - 1u) / RTN_CT_CHUNK;
+  const rtn_u32 gi = c * 4u + (lane & 3u);
+  const rtn_u64 word = gi < nw ? a.fwd_bm[gi] : 0ull;
+  // streamed once: non-temporal, so the occupancy bitmap keeps its place in L2
+  cv[0] = __builtin_nontemporal_load(a.conn + (rtn_u64)c * 64u + lane);
 #pragma unroll
-  for (rtn_u32 u = 0; u < G; ++u) pre[u] = 0u;
+  for (int j = 0; j < 4; ++j) ch.w[j] = rtn_ct_rl64(word, j);
+  const rtn_u32 p[4] = {(rtn_u32)__popcll(ch.w[0]), (rtn_u32)__popcll(ch.w[1]), (rtn_u32)__popcll(ch.w[2]),
+                        (rtn_u32)__popcll(ch.w[3])};
+  ch.p0 = p[0];
+  ch.p01 = p[0] + p[1];
+  ch.p012 = ch.p01 + p[2];
+  ch.total = ch.p012 + p[3];
 #pragma unroll
-  for (rtn_u32 j = 0; j < RTN_CT_GROUPS; ++j) {
-    const rtn_u32 pj = __shfl(pop, (int)j);
-#pragma unroll
-    for (rtn_u32 u = 0; u < G; ++u) pre[u] += j < w * G + u ? pj : 0u;
+  for (rtn_u32 j = 1; j < RTN_CT_PASSES; ++j) {
+    cv[j] = 0ull;
+    if (64u * j + lane < ch.total) cv[j] = __builtin_nontemporal_load(a.conn + rtn_ct_rslot(ch, 64u * j + lane));
   }
-  rtn_u64 m6[G];
+  const rtn_u64 lane_lt = lane ? (~0ull >> (64u - lane)) : 0ull;
+  rtn_u32 v6before = 0u;
 #pragma unroll
-  for (rtn_u32 u = 0; u < G; ++u) {
-    const rtn_u32 q = w * G + u;  // group within the chunk
-    const rtn_u64 m = __shfl(word, (int)q);
-    f.has[u] = c * (RTN_CT_CHUNK / 64u) + q < nw && ((m >> lane) & 1ull);
-    // record slot (RTN_REC_INDEX, retina_pc.h): block k / 64 of chunk c at block slot
-    // (k / 64) * nchunks + c
-    const rtn_u32 k = pre[u] + (rtn_u32)__popcll(m & lane_lt);
-    f.r[u] = ((rtn_u64)(k >> 6) * nch + c) * 64u + (k & 63u);
-    f.frame[u] = (c * (RTN_CT_CHUNK / 64u) + q) * 64u + lane;
-#pragma unroll
-    for (int j = 0; j < 6; ++j) f.rec[u][j] = 0u;
-    // streamed once: non-temporal, so the occupancy bitmap keeps its place in L2. The record
-    // itself is read only by frames that need their key (rtn_ct_load_rec): rtn_conn_t carries
-    // the IPv6 and UDP bits the rest needs.
-    f.cv[u] = f.has[u] ? __builtin_nontemporal_load(a.conn + f.r[u]) : 0ull;
+  for (rtn_u32 j = 0; j < RTN_CT_PASSES; ++j) {
+    has[j] = 64u * j + lane < ch.total;
+    if (!has[j]) cv[j] = 0ull;
+    const rtn_u64 m6 = __ballot(has[j] && ((cv[j] >> 61) & 1ull));  // RTN_CONN_IPV6
+    v6r[j] = v6before + (rtn_u32)__popcll(m6 & lane_lt);
+    v6before += (rtn_u32)__popcll(m6);
   }
+}
+
+// A record the table step needs, staged in LDS: its rank k, IPv6 rank, rtn_conn_t.
+struct rtn_ct_item {
+  rtn_u64 cv;
+  rtn_u32 k, v6r;
+};
+
+// Appends the lanes with `take` of every pass to the wave's list; returns the list length.
+__device__ __forceinline__ rtn_u32 rtn_ct_compact(rtn_ct_item* list, rtn_u32 lane, const bool (&take)[RTN_CT_PASSES],
+                                                  const rtn_u64 (&cv)[RTN_CT_PASSES],
+                                                  const rtn_u32 (&v6r)[RTN_CT_PASSES]) {
+  const rtn_u64 lane_lt = lane ? (~0ull >> (64u - lane)) : 0ull;
+  rtn_u32 cnt = 0u;
 #pragma unroll
-  for (rtn_u32 u = 0; u < G; ++u) {
-    m6[u] = __ballot(f.has[u] && ((f.cv[u] >> 61) & 1ull));  // RTN_CONN_IPV6
-    if (lane == 0u) v6cnt[w * G + u] = (rtn_u32)__popcll(m6[u]);
+  for (rtn_u32 j = 0; j < RTN_CT_PASSES; ++j) {
+    const rtn_u64 m = __ballot(take[j]);
+    if (take[j]) {
+      rtn_ct_item& it = list[cnt + (rtn_u32)__popcll(m & lane_lt)];
+      it.cv = cv[j];
+      it.k = 64u * j + lane;
+      it.v6r = v6r[j];
+    }
+    cnt += (rtn_u32)__popcll(m);
+  }
+  return cnt;
+}
+
+// The record (4 words) of item `it` and its key.
+__device__ __forceinline__ void rtn_ct_item_key(const rtn_ct_args& a, const rtn_ct_chunk& ch, const rtn_ct_item& it,
+                                                rtn_ct_key& k) {
+  const rtn_u64* rp = reinterpret_cast<const rtn_u64*>(a.recs + rtn_ct_rslot(ch, it.k) * 4u);
+  rtn_u32 rec[4];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const rtn_u64 x = __builtin_nontemporal_load(rp + j);
+    rec[2 * j] = (rtn_u32)x;
+    rec[2 * j + 1] = (rtn_u32)(x >> 32);
+  }
+  const bool v6 = (it.cv >> 61) & 1ull;
+  rtn_ct_make_key(a, rec, it.cv, v6 ? a.addr6 + ((rtn_u64)ch.c * RTN_CT_CHUNK + it.v6r) * 8u : nullptr, k);
+}
+
+extern "C" __global__ void __launch_bounds__(64u * RTN_CT_CPB) rtn_ct_insert(rtn_ct_args a) {
+  __shared__ rtn_u32 blk[4];  // openers needing a new slot (then tickets drawn), reservation base, granted, rounds
+  __shared__ rtn_ct_item lists[RTN_CT_CPB][RTN_CT_CHUNK];
+  const rtn_u32 lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  const rtn_u32 c = blockIdx.x * RTN_CT_CPB + wv;
+  const rtn_u32 nch = (a.n + RTN_CT_CHUNK - 1u) / RTN_CT_CHUNK;
+  if (threadIdx.x == 0) {
+    blk[0] = 0u;
+    blk[3] = 0u;
+  }
+  rtn_ct_item* list = lists[wv];
+  rtn_ct_chunk ch;
+  rtn_u64 cv[RTN_CT_PASSES];
+  bool has[RTN_CT_PASSES], op[RTN_CT_PASSES];
+  rtn_u32 v6r[RTN_CT_PASSES];
+  rtn_u32 nop = 0u;
+  if (c < nch) {  // wave-uniform
+    rtn_ct_begin(a, c, lane, ch, cv, has, v6r);
+#pragma unroll
+    for (rtn_u32 j = 0; j < RTN_CT_PASSES; ++j) {
+      // openers: creates, and not a TCP opener dropped by filter_first_packet
+      const rtn_u32 info = (rtn_u32)(cv[j] >> 32);
+      const bool tcp = !((info >> 30) & 1u);  // RTN_CONN_UDP
+      op[j] = has[j] && ((info >> 26) & 1u) && !(tcp && (info & 0x3ffffffu) == 0u);
+    }
+    nop = rtn_ct_compact(list, lane, op, cv, v6r);
   }
   __syncthreads();
-#pragma unroll
-  for (rtn_u32 u = 0; u < G; ++u) {
-    const rtn_u32 q = w * G + u;
-    rtn_u32 v6base = 0u;
-    for (rtn_u32 j = 0; j < q; ++j) v6base += v6cnt[j];
-    const rtn_u64 v6r = (rtn_u64)c * RTN_CT_CHUNK + v6base + (rtn_u32)__popcll(m6[u] & lane_lt);
-    f.a6[u] = (m6[u] >> lane) & 1ull ? a.addr6 + v6r * 8u : nullptr;
-  }
-}
-
-// The record of group u's frame (for its key).
-__device__ __forceinline__ void rtn_ct_load_rec(const rtn_ct_args& a, rtn_ct_frames& f, rtn_u32 u) {
-  const rtn_u64* rp = reinterpret_cast<const rtn_u64*>(a.recs + f.r[u] * 6u);  // 8-byte aligned
-#pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    const rtn_u64 x = __builtin_nontemporal_load(rp + j);
-    f.rec[u][2 * j] = (rtn_u32)x;
-    f.rec[u][2 * j + 1] = (rtn_u32)(x >> 32);
-  }
-}
-
-extern "C" __global__ void __launch_bounds__(64u * RTN_CT_WPC * RTN_CT_INSERT_CPB) rtn_ct_insert(rtn_ct_args a) {
-  constexpr rtn_u32 G = RTN_CT_GPW;
-  __shared__ rtn_u32 blk[3];  // openers needing a new slot (then tickets drawn), reservation base, granted
-  if (threadIdx.x == 0) blk[0] = 0u;
-  rtn_ct_frames f;
-  rtn_ct_load<RTN_CT_INSERT_CPB>(a, f);
-  const rtn_u32 lane = threadIdx.x & 63u;
-  bool active[G];
-  rtn_u32 slot[G];
-  rtn_ct_key k[G];
-#pragma unroll
-  for (rtn_u32 u = 0; u < G; ++u) {
-    // openers: creates, and not a TCP opener dropped by filter_first_packet
-    const rtn_u32 info = (rtn_u32)(f.cv[u] >> 32);
-    const bool tcp = !((info >> 30) & 1u);  // RTN_CONN_UDP
-    active[u] = f.has[u] && ((info >> 26) & 1u) && !(tcp && (info & 0x3ffffffu) == 0u);
-    if (active[u]) rtn_ct_load_rec(a, f, u);
-    slot[u] = (rtn_u32)f.cv[u] & a.cap_mask;
-  }
-#pragma unroll
-  for (rtn_u32 u = 0; u < G; ++u)
-    if (active[u]) rtn_ct_make_key(a, f.rec[u], f.cv[u], f.a6[u], k[u]);
-  // Phase A: find the key or the first empty slot of its probe chain (no writes), remembering the
-  // chain's first removed slot: a key known to be absent reuses it, so that removals do not
-  // leave the chains to fill up with tombstones until a rebuild.
-  bool at_empty[G];
-  rtn_u32 tomb[G];
-#pragma unroll
-  for (rtn_u32 u = 0; u < G; ++u) {
-    at_empty[u] = false;
-    tomb[u] = 0xffffffffu;
-  }
-  for (rtn_u32 p = 0; p < RTN_CT_MAXPROBE; ++p) {
-    bool more = false;
-#pragma unroll
-    for (rtn_u32 u = 0; u < G; ++u) {
-      if (active[u] && !at_empty[u]) {
-        const rtn_u64 t = rtn_ct_occupied(a.occ, slot[u])
-                              ? __hip_atomic_load(rtn_ct_tag(a, slot[u]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+  // every wave runs the block's largest number of 64-opener rounds (the admission below takes
+  // block-wide barriers)
+  if (lane == 0u && nop) atomicMax(&blk[3], (nop + 63u) / 64u);
+  __syncthreads();
+  const rtn_u32 rounds = blk[3];
+  for (rtn_u32 rd = 0; rd < rounds; ++rd) {
+    const rtn_u32 e = rd * 64u + lane;
+    bool active = e < nop;
+    rtn_ct_item it = {0ull, 0u, 0u};
+    rtn_ct_key k;
+    rtn_u32 slot = 0u, frame = 0u;
+    if (active) {
+      it = list[e];
+      rtn_ct_item_key(a, ch, it, k);
+      slot = (rtn_u32)it.cv & a.cap_mask;
+      frame = rtn_ct_frame(ch, it.k);
+    }
+    // Phase A: find the key or the first empty slot of its probe chain (no writes), remembering the
+    // chain's first removed slot: a key known to be absent reuses it, so that removals do not
+    // leave the chains to fill up with tombstones until a rebuild.
+    bool at_empty = false;
+    rtn_u32 tomb = 0xffffffffu;
+    for (rtn_u32 p = 0; p < RTN_CT_MAXPROBE; ++p) {
+      bool more = false;
+      if (active && !at_empty) {
+        const rtn_u64 t = rtn_ct_occupied(a.occ, slot)
+                              ? __hip_atomic_load(rtn_ct_tag(a, slot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                               : RTN_CT_EMPTY;
-        if (t == k[u].fp) {
+        if (t == k.fp) {
           // `first` only matters for a slot opened in this batch (epoch == this batch, or 0 while
           // its claimer is still writing it); an older connection's frames are plain hits
-          const rtn_u32 ep = a.table[(rtn_u64)slot[u] * 16u + 2u];
-          if (ep == 0u || ep == a.epoch) atomicMin(&a.table[(rtn_u64)slot[u] * 16u + 3u], f.frame[u]);
-          active[u] = false;
+          const rtn_u32 ep = a.table[(rtn_u64)slot * 16u + 2u];
+          if (ep == 0u || ep == a.epoch) atomicMin(&a.table[(rtn_u64)slot * 16u + 3u], frame);
+          active = false;
         } else if (t == RTN_CT_EMPTY) {
-          at_empty[u] = true;
+          at_empty = true;
         } else {
-          if (t == RTN_CT_REMOVED && tomb[u] == 0xffffffffu) tomb[u] = slot[u];
-          slot[u] = (slot[u] + 1u) & a.cap_mask;
+          if (t == RTN_CT_REMOVED && tomb == 0xffffffffu) tomb = slot;
+          slot = (slot + 1u) & a.cap_mask;
           more = true;
         }
       }
+      if (!__ballot(more)) break;
     }
-    if (!__ballot(more)) break;
-  }
-  rtn_u32 want = 0u;
-#pragma unroll
-  for (rtn_u32 u = 0; u < G; ++u) {
-    active[u] = active[u] && at_empty[u];  // probe limit reached without an empty slot: full
-    if (active[u] && tomb[u] != 0xffffffffu) slot[u] = tomb[u];  // claim from the first removed slot
-    want += (rtn_u32)__popcll(__ballot(active[u]));
-  }
-  // Admission (ConnTracker's size < max_connections): the block reserves one ticket per opener
-  // that still needs a slot with a single atomic (none once its connections exist) and returns
-  // the unused tickets at the end.
-  if (a.check) {
-    if (lane == 0u && want) atomicAdd(&blk[0], want);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      const rtn_u32 all = blk[0];
-      const rtn_u32 b = all ? atomicAdd(&a.live[0], all) : 0u;
-      blk[1] = all;
-      blk[2] = b >= a.max_live ? 0u : (a.max_live - b < all ? a.max_live - b : all);
-      blk[0] = 0u;
+    active = active && at_empty;  // probe limit reached without an empty slot: full
+    if (active && tomb != 0xffffffffu) slot = tomb;  // claim from the first removed slot
+    const rtn_u32 want = (rtn_u32)__popcll(__ballot(active));
+    // Admission (ConnTracker's size < max_connections): the block reserves one ticket per opener
+    // that still needs a slot with a single atomic (none once its connections exist) and returns
+    // the unused tickets at the end.
+    if (a.check) {
+      __syncthreads();
+      if (threadIdx.x == 0) blk[0] = 0u;
+      __syncthreads();
+      if (lane == 0u && want) atomicAdd(&blk[0], want);
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        const rtn_u32 all = blk[0];
+        const rtn_u32 b = all ? atomicAdd(&a.live[0], all) : 0u;
+        blk[1] = all;
+        blk[2] = b >= a.max_live ? 0u : (a.max_live - b < all ? a.max_live - b : all);
+        blk[0] = 0u;
+      }
+      __syncthreads();
+      const rtn_u32 ticket = active ? atomicAdd(&blk[0], 1u) : 0u;
+      if (active && ticket >= blk[2]) active = false;  // table full for this opener
     }
-    __syncthreads();
-#pragma unroll
-    for (rtn_u32 u = 0; u < G; ++u) {
-      const rtn_u32 ticket = active[u] ? atomicAdd(&blk[0], 1u) : 0u;
-      if (active[u] && ticket >= blk[2]) active[u] = false;  // table full for this opener
-    }
-  }
-  // Phase B: claim from the first free (empty or removed) slot on (another lane may take it
-  // first: keep probing). A removed slot was reset to epoch 0 / first 0xffffffff by its removal,
-  // so until its claimer has written the epoch, lanes of the same key lower `first` (phase A).
-  rtn_u32 claims = 0u;
-  for (rtn_u32 p = 0; p < RTN_CT_MAXPROBE; ++p) {
-    bool more = false;
-#pragma unroll
-    for (rtn_u32 u = 0; u < G; ++u) {
-      if (active[u]) {
-        rtn_u64* tag = rtn_ct_tag(a, slot[u]);
+    // Phase B: claim from the first free (empty or removed) slot on (another lane may take it
+    // first: keep probing). A removed slot was reset to epoch 0 / first 0xffffffff by its removal,
+    // so until its claimer has written the epoch, lanes of the same key lower `first` (phase A).
+    rtn_u32 claims = 0u;
+    for (rtn_u32 p = 0; p < RTN_CT_MAXPROBE; ++p) {
+      bool more = false;
+      if (active) {
+        rtn_u64* tag = rtn_ct_tag(a, slot);
         rtn_u64 t = __hip_atomic_load(tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const rtn_u64 seen = t;
-        if (t <= RTN_CT_REMOVED) t = atomicCAS(tag, seen, k[u].fp);
+        if (t <= RTN_CT_REMOVED) t = atomicCAS(tag, seen, k.fp);
         if (t == seen && seen <= RTN_CT_REMOVED) {
-          atomicOr(&a.occ[slot[u] >> 5], 1u << (slot[u] & 31u));
-          rtn_u32* s = a.table + (rtn_u64)slot[u] * 16u;
+          atomicOr(&a.occ[slot >> 5], 1u << (slot & 31u));
+          rtn_u32* s = a.table + (rtn_u64)slot * 16u;
           s[2] = a.epoch;
 #pragma unroll
-          for (int j = 0; j < 10; ++j) s[4 + j] = k[u].w[j];
-          atomicMin(&s[3], f.frame[u]);
-          active[u] = false;
+          for (int j = 0; j < 10; ++j) s[4 + j] = k.w[j];
+          atomicMin(&s[3], frame);
+          active = false;
           ++claims;
-        } else if (t == k[u].fp) {
-          atomicMin(&a.table[(rtn_u64)slot[u] * 16u + 3u], f.frame[u]);
-          active[u] = false;
+        } else if (t == k.fp) {
+          atomicMin(&a.table[(rtn_u64)slot * 16u + 3u], frame);
+          active = false;
         } else {
-          slot[u] = (slot[u] + 1u) & a.cap_mask;
+          slot = (slot + 1u) & a.cap_mask;
           more = true;
         }
       }
+      if (!__ballot(more)) break;
     }
-    if (!__ballot(more)) break;
-  }
-  rtn_u32 n = claims;
+    rtn_u32 nclaim = claims;
 #pragma unroll
-  for (int d = 1; d < 64; d <<= 1) n += __shfl_xor(n, d);
-  if (a.check) {
-    // return the reserved tickets that did not become a connection
-    __syncthreads();
-    if (threadIdx.x == 0) blk[0] = 0u;
-    __syncthreads();
-    if (lane == 0u && n) atomicAdd(&blk[0], n);
-    __syncthreads();
-    if (threadIdx.x == 0 && blk[1] > blk[0]) atomicSub(&a.live[0], blk[1] - blk[0]);
-  } else if (lane == 0u && n) {
-    // one atomic per wave, spread over 64 counters (live = their sum)
-    atomicAdd(&a.live[(blockIdx.x * 8u + (threadIdx.x >> 6)) & 63u], n);
+    for (int d = 1; d < 64; d <<= 1) nclaim += __shfl_xor(nclaim, d);
+    if (a.check) {
+      // return the reserved tickets that did not become a connection
+      __syncthreads();
+      if (threadIdx.x == 0) blk[0] = 0u;
+      __syncthreads();
+      if (lane == 0u && nclaim) atomicAdd(&blk[0], nclaim);
+      __syncthreads();
+      if (threadIdx.x == 0 && blk[1] > blk[0]) atomicSub(&a.live[0], blk[1] - blk[0]);
+    } else if (lane == 0u && nclaim) {
+      // one atomic per wave, spread over 64 counters (live = their sum)
+      atomicAdd(&a.live[(blockIdx.x * 8u + wv) & 63u], nclaim);
+    }
   }
 }
 
@@ -378,85 +439,87 @@ __device__ __forceinline__ rtn_u32 rtn_ct_status(const rtn_ct_args& a, rtn_u32 e
   return frame > first ? RTN_CT_HIT : frame == first ? RTN_CT_NEW : (opens ? RTN_CT_NEW_DROPPED : RTN_CT_MISS);
 }
 
-extern "C" __global__ void __launch_bounds__(64u * RTN_CT_WPC * RTN_CT_LOOKUP_CPB) rtn_ct_lookup(rtn_ct_args a) {
-  constexpr rtn_u32 G = RTN_CT_GPW;
-  rtn_ct_frames f;
-  rtn_ct_load<RTN_CT_LOOKUP_CPB>(a, f);
-  // Every group's first probe is issued before any is used: the start slot's occupancy bit (in
-  // L2; most misses end here), then the tags of occupied start slots, then the slots whose tag
-  // matches. Only chains (start slot held by another key or removed) probe further, one by one.
-  bool occ0[G];
+// outcome of a frame whose key is not in the table
+__device__ __forceinline__ rtn_u32 rtn_ct_absent(rtn_u64 cv) {
+  const rtn_u32 info = (rtn_u32)(cv >> 32);
+  const bool opens = (info >> 26) & 1u;
+  const bool dropped = !((info >> 30) & 1u) && (info & 0x3ffffffu) == 0u;  // TCP opener the filter drops
+  return !opens ? RTN_CT_MISS : dropped ? RTN_CT_NEW_DROPPED : RTN_CT_FULL;
+}
+
+extern "C" __global__ void __launch_bounds__(64u * RTN_CT_CPB) rtn_ct_lookup(rtn_ct_args a) {
+  __shared__ rtn_ct_item lists[RTN_CT_CPB][RTN_CT_CHUNK];
+  const rtn_u32 lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  const rtn_u32 c = blockIdx.x * RTN_CT_CPB + wv;
+  const rtn_u32 nch = (a.n + RTN_CT_CHUNK - 1u) / RTN_CT_CHUNK;
+  if (c >= nch) return;  // wave-uniform (no block barriers below)
+  rtn_ct_item* list = lists[wv];
+  rtn_ct_chunk ch;
+  rtn_u64 cv[RTN_CT_PASSES];
+  bool has[RTN_CT_PASSES], occ0[RTN_CT_PASSES];
+  rtn_u32 v6r[RTN_CT_PASSES];
+  rtn_ct_begin(a, c, lane, ch, cv, has, v6r);
+  // the start slot's occupancy bit (in L2) settles most frames: a clear bit is a miss
 #pragma unroll
-  for (rtn_u32 u = 0; u < G; ++u) {
-    occ0[u] = f.has[u] && rtn_ct_occupied(a.occ, (rtn_u32)f.cv[u] & a.cap_mask);
-  }
-  // an occupied start slot is read whole (tag, epoch, first, key: one 64-B line) in one go
-  rtn_ct_key k[G];
-  rtn_u64 t[G];
-  uint4 s0[G], s1[G], s2[G];  // words 0-11 (tag, epoch, first, key 0-7); key 8-9 in s3
-  uint2 s3[G];
+  for (rtn_u32 j = 0; j < RTN_CT_PASSES; ++j) occ0[j] = has[j] && rtn_ct_occupied(a.occ, (rtn_u32)cv[j] & a.cap_mask);
 #pragma unroll
-  for (rtn_u32 u = 0; u < G; ++u) {
-    t[u] = RTN_CT_EMPTY;
-    if (occ0[u]) {
-      const uint4* sp = reinterpret_cast<const uint4*>(a.table + (rtn_u64)((rtn_u32)f.cv[u] & a.cap_mask) * 16u);
-      s0[u] = sp[0];
-      s1[u] = sp[1];
-      s2[u] = sp[2];
-      s3[u] = reinterpret_cast<const uint2*>(sp + 3)[0];
-      rtn_ct_load_rec(a, f, u);
-    }
-  }
-#pragma unroll
-  for (rtn_u32 u = 0; u < G; ++u) {
-    if (occ0[u]) {
-      rtn_ct_make_key(a, f.rec[u], f.cv[u], f.a6[u], k[u]);
-      t[u] = (rtn_u64)s0[u].x | ((rtn_u64)s0[u].y << 32);
-    }
-  }
-#pragma unroll
-  for (rtn_u32 u = 0; u < G; ++u) {
-    if (!f.has[u]) continue;
-    const rtn_u64 cv = f.cv[u];
-    const rtn_u32 info = (rtn_u32)(cv >> 32), frame = f.frame[u];
-    const bool opens = (info >> 26) & 1u;
-    const bool dropped = !((info >> 30) & 1u) && (info & 0x3ffffffu) == 0u;  // TCP opener the filter drops
-    rtn_u32 slot = (rtn_u32)cv & a.cap_mask, status = 0u, found = 0xffffffffu;
-    if (occ0[u] && t[u] == k[u].fp) {
-      const rtn_u32 w[10] = {s1[u].x, s1[u].y, s1[u].z, s1[u].w, s2[u].x, s2[u].y, s2[u].z, s2[u].w, s3[u].x, s3[u].y};
+  for (rtn_u32 j = 0; j < RTN_CT_PASSES; ++j)
+    if (has[j] && !occ0[j])
+      __builtin_nontemporal_store((rtn_u64)RTN_CT_NO_SLOT_K | ((rtn_u64)rtn_ct_absent(cv[j]) << 32),
+                                  a.out + rtn_ct_rslot(ch, 64u * j + lane));
+  const rtn_u32 nocc = rtn_ct_compact(list, lane, occ0, cv, v6r);
+  rtn_ct_wave_sync();
+  // The frames whose start slot is occupied, 64 at a time: the slot is read whole (tag, epoch,
+  // first, key: one 64-B line) together with the record; only chains walk further.
+  for (rtn_u32 e0 = 0; e0 < nocc; e0 += 64u) {
+    const rtn_u32 e = e0 + lane;
+    if (e >= nocc) break;
+    const rtn_ct_item it = list[e];
+    rtn_u32 slot = (rtn_u32)it.cv & a.cap_mask;
+    const uint4* sp = reinterpret_cast<const uint4*>(a.table + (rtn_u64)slot * 16u);
+    const uint4 s0 = sp[0], s1 = sp[1], s2 = sp[2];
+    const uint2 s3 = reinterpret_cast<const uint2*>(sp + 3)[0];
+    rtn_ct_key k;
+    rtn_ct_item_key(a, ch, it, k);
+    const rtn_u32 frame = rtn_ct_frame(ch, it.k);
+    const bool opens = (it.cv >> 58) & 1ull;  // RTN_CONN_CREATES (info bit 26)
+    const rtn_u64 t = (rtn_u64)s0.x | ((rtn_u64)s0.y << 32);
+    rtn_u32 status = 0u, found = RTN_CT_NO_SLOT_K;
+    if (t == k.fp) {
+      const rtn_u32 w[10] = {s1.x, s1.y, s1.z, s1.w, s2.x, s2.y, s2.z, s2.w, s3.x, s3.y};
       bool same = true;
 #pragma unroll
-      for (int j = 0; j < 10; ++j) same = same && w[j] == k[u].w[j];
+      for (int j = 0; j < 10; ++j) same = same && w[j] == k.w[j];
       if (same) {
         found = slot;
-        status = rtn_ct_status(a, s0[u].z, s0[u].w, frame, opens);
+        status = rtn_ct_status(a, s0.z, s0.w, frame, opens);
       } else {
         status = RTN_CT_COLLISION;
       }
-    } else if (occ0[u] && t[u] != RTN_CT_EMPTY) {
+    } else if (t != RTN_CT_EMPTY) {
       // the start slot holds another key (or was removed): walk the chain
       for (rtn_u32 p = 1; p < RTN_CT_MAXPROBE; ++p) {
         slot = (slot + 1u) & a.cap_mask;
         if (!rtn_ct_occupied(a.occ, slot)) break;
-        const rtn_u32* sp = a.table + (rtn_u64)slot * 16u;
-        const rtn_u64 tt = *reinterpret_cast<const rtn_u64*>(sp);
+        const rtn_u32* q = a.table + (rtn_u64)slot * 16u;
+        const rtn_u64 tt = *reinterpret_cast<const rtn_u64*>(q);
         if (tt == RTN_CT_EMPTY) break;
-        if (tt != k[u].fp) continue;
+        if (tt != k.fp) continue;
         bool same = true;
 #pragma unroll
-        for (int j = 0; j < 10; ++j) same = same && sp[4 + j] == k[u].w[j];
+        for (int j = 0; j < 10; ++j) same = same && q[4 + j] == k.w[j];
         if (!same) {
           status = RTN_CT_COLLISION;
           break;
         }
         found = slot;
-        status = rtn_ct_status(a, sp[2], sp[3], frame, opens);
+        status = rtn_ct_status(a, q[2], q[3], frame, opens);
         break;
       }
     }
-    if (status == 0u) status = !opens ? RTN_CT_MISS : dropped ? RTN_CT_NEW_DROPPED : RTN_CT_FULL;
-    if (status == RTN_CT_COLLISION) found = 0xffffffffu;
-    __builtin_nontemporal_store((rtn_u64)found | ((rtn_u64)status << 32), a.out + f.r[u]);
+    if (status == 0u) status = rtn_ct_absent(it.cv);
+    if (status == RTN_CT_COLLISION) found = RTN_CT_NO_SLOT_K;
+    __builtin_nontemporal_store((rtn_u64)found | ((rtn_u64)status << 32), a.out + rtn_ct_rslot(ch, it.k));
   }
 }
 

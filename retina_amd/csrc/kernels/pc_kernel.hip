@@ -49,14 +49,15 @@ typedef unsigned int rtn_v4u __attribute__((ext_vector_type(4)));
 // line four times and stay plain).
 #define RTN_LD_STREAM(p) __builtin_nontemporal_load(p)
 
-struct rtn_l4rec {       // 24 B, the compacted L4Context of a forwarded packet (rtn_l4ctx_t)
-  rtn_u32 src_ip4;       // u32::from(Ipv4Addr) (0 for IPv6; addresses in addr6 side array)
-  rtn_u32 dst_ip4;
+struct rtn_l4rec {       // 16 B, the compacted L4Context of a forwarded packet (rtn_l4ctx_t)
+  rtn_u32 w0;            // IPv4: u32::from(src Ipv4Addr); IPv6 TCP: seq_no; IPv6 UDP: 0
+  rtn_u32 w1;            // IPv4: dst; IPv6 TCP: ack_no; IPv6 UDP: 0
   rtn_u32 ports;         // src_port | dst_port << 16
-  rtn_u32 seq_no;        // TCP only
-  rtn_u32 ack_no;        // TCP only
   rtn_u32 meta;          // offset >> 2 | udp << 6 | ipv6 << 7 | tcp flags << 8 | length << 16
 };
+// IPv4 TCP records keep seq_no | ack_no << 32 in the tcp4 side stream (rtn_pc_out_t.tcp4), ranked
+// among the chunk's IPv4 TCP records: no record carries a field that is always zero for its kind
+// (UDP has no seq/ack, IPv6 keeps its addresses in addr6; pdu.rs:66-84).
 
 struct rtn_args {
   const unsigned char* slab;
@@ -64,10 +65,10 @@ struct rtn_args {
   const unsigned short* dlen;
   rtn_u32 n;
   rtn_u32 flags;              // bit0: addr6, bit1: counters, bit2: conn, bit3: caller asserts data_len <= 64,
-                              // bit4: compact ext rows (RTN_BATCH_EXT_COMPACT)
+                              // bit4: compact ext rows (RTN_BATCH_EXT_COMPACT), bit5: tcp4
   rtn_u64* pc_bm;             // [ceil(n/64)]  PacketContinue bit
   rtn_u64* fwd_bm;            // [ceil(n/64)]  PacketContinue && L4Context::new Ok
-  rtn_l4rec* recs;            // [ceil(n/256)*256], dense per chunk
+  rtn_l4rec* recs;            // [ceil(n/256)*256] at RTN_REC_INDEX
   unsigned char* addr6;       // [ceil(n/256)*256][32] (rtn_out_addr6_bytes) (src, dst) raw bytes, IPv6
                               // records only; rtn_flush6 pads a chunk's last store to whole lines,
                               // up to 3 entries past its last record (inside the chunk's 256)
@@ -81,6 +82,8 @@ struct rtn_args {
   const rtn_u32* ext_chunk;   // flags bit4 (compact ext): row of each chunk's first needing frame
   rtn_u32 ext_rows;           // ... and the rows ext holds
   rtn_u32 cpw;                // compact split kernel: consecutive chunks per wave (1 or 2)
+  rtn_u64* tcp4;              // optional [ceil(n/256)*256] seq | ack << 32 of the IPv4 TCP records, at
+                              // RTN_REC_INDEX of their rank among the chunk's IPv4 TCP records (bit5)
 };
 
 struct rtn_view {
@@ -346,6 +349,7 @@ struct rtn_chunk {
   rtn_u32 ndlv;             // delivery records produced in this chunk
   rtn_u32 nv6, nv6flushed;  // IPv6 address records (addr6) produced / stored in this chunk
   rtn_u32 next;             // compact ext: needing frames of this chunk so far
+  rtn_u32 ntcp, ntflushed;  // IPv4 TCP records (tcp4 side stream) produced / stored in this chunk
   rtn_u64 my_pc, my_fwd, my_dlv;  // lane k holds group k's bitmap words until the chunk ends
 };
 
@@ -363,35 +367,43 @@ __device__ __forceinline__ rtn_u64 rtn_rec_slot(rtn_u64 nch, rtn_u64 c, rtn_u32 
 }
 
 
-// Records leave through a per-wave LDS ring of 128 records (3 KB) as whole 64-record blocks:
-// full-width 16-B-per-lane stores, every line written whole.
+// Records leave through a per-wave LDS ring of 128 records (2 KB) as whole 64-record blocks:
+// full-width 16-B-per-lane stores (one record per lane), every line written whole; the IPv4 TCP
+// records' seq/ack through a second ring of 128 8-B entries (1 KB), 64-entry blocks of 512 B.
 #define RTN_RING 128u
 #define RTN_FLUSH 64u
 
 template <bool CONN>
 __device__ __forceinline__ void rtn_flush(const rtn_args& a, const rtn_u64* ring, const rtn_u64* cring,
                                           const rtn_chunk& ch, rtn_u32 lane, rtn_u32 nrecs) {
+  const rtn_u64 nch = rtn_nchunks(a.n);
+  const rtn_u64 c = ch.rec_base / (64u * RTN_CHUNK_GROUPS);
   if (CONN) {
     // connection-stage entries (8 B) share the records' indices: same block, 128-B lines
     const rtn_u32 nc = ((nrecs + 1u) / 2u + 7u) & ~7u;
     // (a block of RTN_RB entries is RTN_RB / 2 lanes; a flush may span several blocks)
     const rtn_v4u* csrc = reinterpret_cast<const rtn_v4u*>(cring + (ch.nflushed & (RTN_RING - 1u)));
-    const rtn_u64 nch = rtn_nchunks(a.n);
-    rtn_v4u* cdst = reinterpret_cast<rtn_v4u*>(a.conn + rtn_rec_slot(nch, ch.rec_base / (64u * RTN_CHUNK_GROUPS), ch.nflushed));
+    rtn_v4u* cdst = reinterpret_cast<rtn_v4u*>(a.conn + rtn_rec_slot(nch, c, ch.nflushed));
     if (lane < nc) RTN_ST(cdst + (lane / (RTN_RB / 2u)) * nch * (RTN_RB / 2u) + lane % (RTN_RB / 2u), csrc[lane]);
   }
-  // whole 128-B lines only: the block starts line-aligned and the tail is padded with stale ring
-  // bytes into the chunk's unused record space (a partial line costs a read-modify-write)
-  const rtn_u32 nv4 = ((nrecs * 3u + 1u) / 2u + 7u) & ~7u;
-  const rtn_v4u* src = reinterpret_cast<const rtn_v4u*>(ring) + ((ch.nflushed & (RTN_RING - 1u)) * 3u >> 1);
-  // a block of RTN_RB records is RTN_RB * 3 / 2 lanes; a flush (RTN_FLUSH) may span several
+  // whole 128-B lines only (8 records): the block starts line-aligned and the tail is padded with
+  // stale ring bytes into the chunk's unused record space (a partial line costs a read-modify-write)
+  const rtn_u32 nl = (nrecs + 7u) & ~7u;
+  const rtn_v4u* src = reinterpret_cast<const rtn_v4u*>(ring) + (ch.nflushed & (RTN_RING - 1u));
+  rtn_v4u* dst = reinterpret_cast<rtn_v4u*>(a.recs + rtn_rec_slot(nch, c, ch.nflushed));
+  // (a block of RTN_RB records is RTN_RB lanes; a flush may span several blocks)
+  if (lane < nl) RTN_ST(dst + (lane / RTN_RB) * nch * RTN_RB + lane % RTN_RB, src[lane]);
+}
+
+// seq/ack entries of IPv4 TCP records [ntflushed, ntflushed + nent): 8 B each, two per lane,
+// whole 128-B lines, 64-entry blocks at RTN_REC_INDEX of the chunk's IPv4-TCP rank.
+__device__ __forceinline__ void rtn_flush_t4(const rtn_args& a, const rtn_u64* ring4, const rtn_chunk& ch,
+                                             rtn_u32 lane, rtn_u32 nent) {
   const rtn_u64 nch = rtn_nchunks(a.n);
-  rtn_v4u* dst = reinterpret_cast<rtn_v4u*>(a.recs + rtn_rec_slot(nch, ch.rec_base / (64u * RTN_CHUNK_GROUPS), ch.nflushed));
-#pragma unroll
-  for (rtn_u32 j = 0; j < 3u; ++j) {
-    const rtn_u32 k = lane + 64u * j;
-    if (k < nv4) RTN_ST(dst + (k / (RTN_RB * 3u / 2u)) * nch * (RTN_RB * 3u / 2u) + k % (RTN_RB * 3u / 2u), src[k]);
-  }
+  const rtn_u32 nl = ((nent + 1u) / 2u + 7u) & ~7u;
+  const rtn_v4u* src = reinterpret_cast<const rtn_v4u*>(ring4 + (ch.ntflushed & (RTN_RING - 1u)));
+  rtn_v4u* dst = reinterpret_cast<rtn_v4u*>(a.tcp4 + rtn_rec_slot(nch, ch.rec_base / (64u * RTN_CHUNK_GROUPS), ch.ntflushed));
+  if (lane < nl) RTN_ST(dst + (lane / (RTN_RB / 2u)) * nch * (RTN_RB / 2u) + lane % (RTN_RB / 2u), src[lane]);
 }
 
 // IPv6 address records (32 B: src, dst) are dense per chunk over the chunk's forwarded IPv6
@@ -425,7 +437,7 @@ __device__ __forceinline__ void rtn_flush6(const rtn_args& a, const rtn_v4u* rin
 template <int NW, bool STAGE6, bool CONN>
 __device__ __forceinline__ void rtn_group(const rtn_args& a, rtn_u32 g, rtn_u32 k, rtn_u32 lane, rtn_u64 lane_lt,
                                           const rtn_u32 (&w)[NW], rtn_u32 dl, rtn_u64* ring, rtn_u64* cring,
-                                          rtn_v4u* ring6, rtn_chunk& ch, rtn_acc& acc) {
+                                          rtn_u64* ring4, rtn_v4u* ring6, rtn_chunk& ch, rtn_acc& acc) {
   const rtn_u32 i = g * 64u + lane;
   const bool valid = i < a.n;
   rtn_view v;
@@ -454,6 +466,9 @@ __device__ __forceinline__ void rtn_group(const rtn_args& a, rtn_u32 g, rtn_u32 
   acc.udpb += (fwd && !v.tcp) ? dl : 0u;
   ch.my_pc = lane == k ? pcm : ch.my_pc;
   ch.my_fwd = lane == k ? fwdm : ch.my_fwd;
+  // IPv4 TCP records: their seq/ack go to the tcp4 side stream (when requested)
+  const bool t4 = fwd && v.v4 && v.tcp && (a.flags & 32u);
+  const rtn_u64 t4m = __ballot(t4);
   if (fwd) {
     const rtn_u32 r = ch.nrec + (rtn_u32)__popcll(fwdm & lane_lt);
     const bool tcp = v.tcp;
@@ -467,10 +482,10 @@ __device__ __forceinline__ void rtn_group(const rtn_args& a, rtn_u32 g, rtn_u32 
     const rtn_u32 src4 = v.v4 ? rtn_l3_be32(v, 12) : 0u, dst4 = v.v4 ? rtn_l3_be32(v, 16) : 0u;
     const rtn_u32 ports = rtn_l4_be16(v, 0) | (rtn_l4_be16(v, 2) << 16);
     const rtn_u32 seq = tcp ? rtn_l4_be32(v, 4) : 0u, ack = tcp ? rtn_l4_be32(v, 8) : 0u;
-    rtn_u64* rp = ring + (r & (RTN_RING - 1u)) * 3u;
-    rp[0] = (rtn_u64)src4 | ((rtn_u64)dst4 << 32);
-    rp[1] = (rtn_u64)ports | ((rtn_u64)seq << 32);
-    rp[2] = (rtn_u64)ack | ((rtn_u64)meta << 32);
+    rtn_u64* rp = ring + (r & (RTN_RING - 1u)) * 2u;
+    rp[0] = v.v4 ? ((rtn_u64)src4 | ((rtn_u64)dst4 << 32)) : ((rtn_u64)seq | ((rtn_u64)ack << 32));
+    rp[1] = (rtn_u64)ports | ((rtn_u64)meta << 32);
+    if (t4) ring4[(ch.ntcp + (rtn_u32)__popcll(t4m & lane_lt)) & (RTN_RING - 1u)] = (rtn_u64)seq | ((rtn_u64)ack << 32);
     if (CONN) {
       // Connection stage of the first packet (conntrack/mod.rs:80-169): ConnId, whether the frame
       // may open a connection (Conn::new_tcp / new_udp, conn/mod.rs:53-96) and the generated
@@ -534,6 +549,7 @@ __device__ __forceinline__ void rtn_group(const rtn_args& a, rtn_u32 g, rtn_u32 
     }
   }
   ch.nrec += nfwd;
+  ch.ntcp += (rtn_u32)__popcll(t4m);
   // IPv6 source/destination addresses, ranked among the chunk's forwarded IPv6 frames
   const bool six = fwd && v.v6 && (a.flags & 1u);
   const rtn_u64 m6 = __ballot(six);
@@ -564,10 +580,18 @@ __device__ __forceinline__ void rtn_group(const rtn_args& a, rtn_u32 g, rtn_u32 
     }
     ch.nv6 += cnt6;
   }
-  if (ch.nrec - ch.nflushed >= RTN_FLUSH) {  // pending < RTN_FLUSH + 64 <= RTN_RING: one block per group
+  // pending < RTN_FLUSH + 64 <= RTN_RING: at most one block per group and ring
+  const bool fr = ch.nrec - ch.nflushed >= RTN_FLUSH, ft = ch.ntcp - ch.ntflushed >= RTN_FLUSH;
+  if (fr || ft) {
     rtn_wave_sync();
-    rtn_flush<CONN>(a, ring, cring, ch, lane, RTN_FLUSH);
-    ch.nflushed += RTN_FLUSH;
+    if (fr) {
+      rtn_flush<CONN>(a, ring, cring, ch, lane, RTN_FLUSH);
+      ch.nflushed += RTN_FLUSH;
+    }
+    if (ft) {
+      rtn_flush_t4(a, ring4, ch, lane, RTN_FLUSH);
+      ch.ntflushed += RTN_FLUSH;
+    }
     rtn_wave_sync();
   }
 #if RTN_DELIVER_WORDS > 0
@@ -609,8 +633,10 @@ __device__ __forceinline__ void rtn_run(const rtn_args& a) {
   const rtn_u64 lane_lt = (lane == 0u) ? 0ull : (~0ull >> (64u - lane));
   constexpr bool slots64 = MODE != RTN_MONO;
   rtn_acc acc = {0u, 0u, 0u, 0u, 0u, 0ull, 0ull, 0ull, 0ull};
-  __shared__ __attribute__((aligned(16))) rtn_u64 rtn_ring[4][RTN_RING * 3u];
+  __shared__ __attribute__((aligned(16))) rtn_u64 rtn_ring[4][RTN_RING * 2u];
   rtn_u64* ring = rtn_ring[threadIdx.x >> 6];
+  __shared__ __attribute__((aligned(16))) rtn_u64 rtn_ring4[4][RTN_RING];  // IPv4 TCP seq/ack
+  rtn_u64* ring4 = rtn_ring4[threadIdx.x >> 6];
   __shared__ __attribute__((aligned(16))) rtn_u64 rtn_cring[4][CONN ? RTN_RING : 2u];  // connection-stage entries
   rtn_u64* cring = rtn_cring[threadIdx.x >> 6];
   constexpr bool stage6 = MODE != RTN_S64;  // 64-byte slots rarely forward IPv6 (only short UDP)
@@ -626,7 +652,7 @@ __device__ __forceinline__ void rtn_run(const rtn_args& a) {
   for (rtn_u32 c = cw; c < cw + cpw && c < nchunks; ++c) {
     const rtn_u32 gb = c * RTN_CHUNK_GROUPS;
     const rtn_u32 ge = gb + RTN_CHUNK_GROUPS < nw ? gb + RTN_CHUNK_GROUPS : nw;
-    rtn_chunk ch = {(rtn_u64)c * (64u * RTN_CHUNK_GROUPS), 0u, 0u, 0u, 0u, 0u, 0u, 0ull, 0ull, 0ull};
+    rtn_chunk ch = {(rtn_u64)c * (64u * RTN_CHUNK_GROUPS), 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0ull, 0ull, 0ull};
     // compact ext: the chunk's first row, read once per chunk (its latency overlaps the first
     // group's loads; read per group it was a dependent round trip in every group)
     const rtn_u32 xrow0 = MODE == RTN_SPLITC ? a.ext_chunk[c] : 0u;
@@ -668,7 +694,7 @@ __device__ __forceinline__ void rtn_run(const rtn_args& a) {
         rtn_load_lo(a, g * 64u + lane, lo, dl);
       }
       if (MODE == RTN_S64) {
-        rtn_group<16, stage6, CONN>(a, g, g - gb, lane, lane_lt, lo, dl, ring, cring, ring6, ch, acc);
+        rtn_group<16, stage6, CONN>(a, g, g - gb, lane, lane_lt, lo, dl, ring, cring, ring4, ring6, ch, acc);
       } else {
         rtn_u32 w[32];
 #pragma unroll
@@ -698,12 +724,13 @@ __device__ __forceinline__ void rtn_run(const rtn_args& a) {
             w[16 + 4 * j + 0] = x.x; w[16 + 4 * j + 1] = x.y; w[16 + 4 * j + 2] = x.z; w[16 + 4 * j + 3] = x.w;
           }
         }
-        rtn_group<32, stage6, CONN>(a, g, g - gb, lane, lane_lt, w, dl, ring, cring, ring6, ch, acc);
+        rtn_group<32, stage6, CONN>(a, g, g - gb, lane, lane_lt, w, dl, ring, cring, ring4, ring6, ch, acc);
       }
     }
     // chunk epilogue: the partial last record block, then one store per bitmap for the chunk
     rtn_wave_sync();
     rtn_flush<CONN>(a, ring, cring, ch, lane, ch.nrec - ch.nflushed);
+    if (ch.ntcp != ch.ntflushed) rtn_flush_t4(a, ring4, ch, lane, ch.ntcp - ch.ntflushed);
     if (stage6) rtn_flush6(a, ring6, ch, lane, ch.nv6 - ch.nv6flushed);
     rtn_wave_sync();
     if (lane < ge - gb) {
@@ -816,7 +843,7 @@ extern "C" __global__ void __launch_bounds__(RTN_PD_THREADS) rtn_pd_kernel(rtn_p
   }
   bool has[G];
   rtn_u64 r[G], cv[G];
-  rtn_u32 rec[G][6], slot[G], st[G];
+  rtn_u32 rec[G][4], slot[G], st[G];
 #pragma unroll
   for (rtn_u32 u = 0; u < G; ++u) {
     const rtn_u32 q = w * G + u;
@@ -824,12 +851,12 @@ extern "C" __global__ void __launch_bounds__(RTN_PD_THREADS) rtn_pd_kernel(rtn_p
     has[u] = ch * RTN_CHUNK_GROUPS + q < nw && ((word >> lane) & 1ull);
     r[u] = rtn_rec_slot(rtn_nchunks(a.n), ch, pre[u] + (rtn_u32)__popcll(word & lane_lt));
 #pragma unroll
-    for (int j = 0; j < 6; ++j) rec[u][j] = 0u;
+    for (int j = 0; j < 4; ++j) rec[u][j] = 0u;
     slot[u] = 0xFFFFFFFFu;
     st[u] = 0u;
     cv[u] = 0ull;
     if (has[u]) {
-      // 16 B per forwarded frame; the 24-B record only for frames that take part (below)
+      // 16 B per forwarded frame; the 16-B record only for frames that take part (below)
       const rtn_u64 e = __builtin_nontemporal_load(reinterpret_cast<const rtn_u64*>(a.ct) + r[u]);
       slot[u] = (rtn_u32)e;
       st[u] = (rtn_u32)(e >> 32);
@@ -850,7 +877,7 @@ extern "C" __global__ void __launch_bounds__(RTN_PD_THREADS) rtn_pd_kernel(rtn_p
       for (int j = 0; j <= RTN_PD_FACTS; ++j) sv[u][j] = sp[j];
       const rtn_u64* rp = reinterpret_cast<const rtn_u64*>(a.recs + r[u]);
 #pragma unroll
-      for (int j = 0; j < 3; ++j) {
+      for (int j = 0; j < 2; ++j) {
         const rtn_u64 x = __builtin_nontemporal_load(rp + j);
         rec[u][2 * j] = (rtn_u32)x;
         rec[u][2 * j + 1] = (rtn_u32)(x >> 32);
@@ -881,10 +908,10 @@ extern "C" __global__ void __launch_bounds__(RTN_PD_THREADS) rtn_pd_kernel(rtn_p
       rtn_cview c;
       c.v6 = v6;
       c.v4 = !v6;
-      c.udp = (rec[u][5] >> 6) & 1u;
+      c.udp = (rec[u][3] >> 6) & 1u;
       c.tcp = !c.udp;
-      c.src4 = rec[u][0];
-      c.dst4 = rec[u][1];
+      c.src4 = v6 ? 0u : rec[u][0];  // (an IPv6 TCP record holds seq / ack there)
+      c.dst4 = v6 ? 0u : rec[u][1];
       c.sport = rec[u][2] & 0xffffu;
       c.dport = rec[u][2] >> 16;
 #pragma unroll
@@ -902,7 +929,7 @@ extern "C" __global__ void __launch_bounds__(RTN_PD_THREADS) rtn_pd_kernel(rtn_p
       }
       // Payload::from_mbuf (datatypes/src/packet.rs:18-29): get_data_slice(offset, length)
       const rtn_u32 dlen = a.dlen[(ch * RTN_CHUNK_GROUPS + q) * 64u + lane];
-      const rtn_u32 off = ((rec[u][5] & 0x3fu) << 2) | 2u, len = rec[u][5] >> 16;
+      const rtn_u32 off = ((rec[u][3] & 0x3fu) << 2) | 2u, len = rec[u][3] >> 16;
       const bool pok = off < dlen && off + len <= dlen;
       rtn_pd_filter(c, pok, &sv[u][1], cnt);
 #pragma unroll

@@ -87,6 +87,20 @@ std::string kernel_template() {
   return kPcKernelSrc;
 }
 
+// The connection-lookup kernel source: the embedded ct_kernel.hip, or (experiments build only)
+// RTN_CT_TEMPLATE=<file>, so that tools/ct_ab.py can time two variants in one process.
+std::string ct_template() {
+#ifdef RTN_EXPERIMENTS
+  if (const char* f = getenv("RTN_CT_TEMPLATE")) {
+    std::ifstream in(f);
+    std::stringstream ss;
+    ss << in.rdbuf();
+    if (in && !ss.str().empty()) return ss.str();
+  }
+#endif
+  return kCtKernelSrc;
+}
+
 std::string env_defines() {
   std::string head;
 #ifdef RTN_EXPERIMENTS
@@ -231,6 +245,7 @@ struct KArgs {
   const uint32_t* ext_chunk;
   uint32_t ext_rows;
   uint32_t cpw;
+  uint64_t* tcp4;
 };
 
 // Groups per wave of a kernel (RTN_PD_GPW / RTN_CT_GPW): the default, unless an RTN_KERNEL_DEFINES
@@ -625,8 +640,8 @@ int32_t rtn_pc_run(rtn_pc_t* pc, const rtn_batch_t* in, rtn_pc_out_t* out, void*
   if (in->stride == 64 && !in->ext && !(in->flags & RTN_BATCH_DL_LE64) && !out->counters)
     return fail(RTN_EINVAL, "64-byte slots without ext need RTN_BATCH_DL_LE64 (every data_len <= 64) or counters");
   // record arrays leave in 16-B-per-lane stores
-  for (const void* o : {(const void*)out->l4, (const void*)out->addr6, (const void*)out->conn})
-    if ((reinterpret_cast<uintptr_t>(o) & 15u) != 0) return fail(RTN_EINVAL, "l4/addr6/conn must be 16-byte aligned");
+  for (const void* o : {(const void*)out->l4, (const void*)out->addr6, (const void*)out->conn, (const void*)out->tcp4})
+    if ((reinterpret_cast<uintptr_t>(o) & 15u) != 0) return fail(RTN_EINVAL, "l4/addr6/conn/tcp4 must be 16-byte aligned");
   const uint32_t dw = pc->program->prog.deliver_words();
   if (dw > 0 && (!out->dlv_bitmap || !out->dlv_records))
     return fail(RTN_EINVAL, "program has packet-level callbacks: dlv_bitmap/dlv_records required");
@@ -644,7 +659,9 @@ int32_t rtn_pc_run(rtn_pc_t* pc, const rtn_batch_t* in, rtn_pc_out_t* out, void*
   a.dlen = in->data_len;
   a.n = in->n;
   a.flags = (out->addr6 ? 1u : 0u) | (out->counters ? 2u : 0u) | (out->conn ? 4u : 0u) |
-            ((in->flags & RTN_BATCH_DL_LE64) ? 8u : 0u) | ((in->flags & RTN_BATCH_EXT_COMPACT) ? 16u : 0u);
+            ((in->flags & RTN_BATCH_DL_LE64) ? 8u : 0u) | ((in->flags & RTN_BATCH_EXT_COMPACT) ? 16u : 0u) |
+            (out->tcp4 ? 32u : 0u);
+  a.tcp4 = out->tcp4;
   a.ext_chunk = in->ext_chunk;
   a.ext_rows = in->ext_rows;
   a.cpw = (in->ext && (in->flags & RTN_BATCH_EXT_COMPACT)) ? (out->conn ? pc->splitc_cpw_conn : pc->splitc_cpw) : 1u;
@@ -764,8 +781,9 @@ int32_t rtn_pc_destroy(rtn_pc_t* pc) {
 // sizes in 64-bit arithmetic (n up to 2^32 - 1 must not wrap)
 size_t rtn_out_bitmap_bytes(uint32_t n) { return (((size_t)n + 63u) / 64u) * 8u; }
 static size_t chunked(uint32_t n) { return (((size_t)n + RTN_CHUNK_FRAMES - 1u) / RTN_CHUNK_FRAMES) * RTN_CHUNK_FRAMES; }
-static_assert(sizeof(rtn_l4ctx_t) == 24, "rtn_l4ctx_t is 24 bytes");
+static_assert(sizeof(rtn_l4ctx_t) == 16, "rtn_l4ctx_t is 16 bytes");
 size_t rtn_out_l4_bytes(uint32_t n) { return chunked(n) * sizeof(rtn_l4ctx_t); }
+size_t rtn_out_tcp4_bytes(uint32_t n) { return chunked(n) * 8u; }
 size_t rtn_out_addr6_bytes(uint32_t n) { return chunked(n) * 32u; }
 size_t rtn_out_dlv_bytes(uint32_t n, uint32_t deliver_words) {
   return chunked(n) * (size_t)deliver_words * 8u;
@@ -801,8 +819,7 @@ struct rtn_ct {
 };
 
 namespace {
-constexpr uint32_t RTN_CT_GPW = 2;  // must match ct_kernel.hip
-constexpr uint32_t RTN_CT_INSERT_CPB = 2, RTN_CT_LOOKUP_CPB = 1;  // chunks per block, must match ct_kernel.hip
+constexpr uint32_t RTN_CT_CPB = 4;  // chunks per block (one wave each), must match ct_kernel.hip
 
 struct CtArgs {  // must match struct rtn_ct_args in ct_kernel.hip
   const uint64_t* fwd_bm;
@@ -853,7 +870,7 @@ int32_t rtn_ct_create(int device, uint32_t capacity_log2, uint32_t max_connectio
   if (!out) return fail(RTN_EINVAL, "null argument");
   if (capacity_log2 < 6 || capacity_log2 > 30) return fail(RTN_EINVAL, "capacity_log2 must be in [6, 30]");
   std::shared_ptr<std::vector<uint8_t>> code;
-  int32_t rc = compile_code_object(env_defines() + kCtKernelSrc, code);
+  int32_t rc = compile_code_object(env_defines() + ct_template(), code);
   if (rc) return rc;
   auto ct = std::make_unique<rtn_ct>();
   ct->device = device;
@@ -922,12 +939,10 @@ int32_t rtn_ct_process(rtn_ct_t* ct, const rtn_pc_out_t* pc, uint32_t n, rtn_ct_
   a.check = spread ? 0u : 1u;
   const uint32_t chunks = (n + RTN_CHUNK_FRAMES - 1u) / RTN_CHUNK_FRAMES;
   void* p[] = {&a};
-  const uint32_t per_chunk = RTN_CHUNK_FRAMES / groups_per_wave("RTN_CT_GPW", RTN_CT_GPW);  // threads
-  const uint32_t iblocks = (chunks + RTN_CT_INSERT_CPB - 1u) / RTN_CT_INSERT_CPB;
-  hipError_t e = hipModuleLaunchKernel(ct->insert, iblocks, 1, 1, per_chunk * RTN_CT_INSERT_CPB, 1, 1, 0, s, p, nullptr);
+  const uint32_t blocks = (chunks + RTN_CT_CPB - 1u) / RTN_CT_CPB;
+  hipError_t e = hipModuleLaunchKernel(ct->insert, blocks, 1, 1, 64u * RTN_CT_CPB, 1, 1, 0, s, p, nullptr);
   if (e != hipSuccess) return hip_fail("rtn_ct_insert", e);
-  const uint32_t lblocks = (chunks + RTN_CT_LOOKUP_CPB - 1u) / RTN_CT_LOOKUP_CPB;
-  e = hipModuleLaunchKernel(ct->lookup, lblocks, 1, 1, per_chunk * RTN_CT_LOOKUP_CPB, 1, 1, 0, s, p, nullptr);
+  e = hipModuleLaunchKernel(ct->lookup, blocks, 1, 1, 64u * RTN_CT_CPB, 1, 1, 0, s, p, nullptr);
   if (e != hipSuccess) return hip_fail("rtn_ct_lookup", e);
   return RTN_OK;
 }

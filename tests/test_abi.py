@@ -78,12 +78,13 @@ def test_output_sizes():
     assert L.rtn_out_bitmap_bytes(65) == 16
     CF = pc.CHUNK_FRAMES
     assert CF == 256
-    assert L.rtn_out_l4_bytes(65) == CF * 24
-    assert L.rtn_out_l4_bytes(1025) == 1280 * 24
+    assert L.rtn_out_l4_bytes(65) == CF * 16
+    assert L.rtn_out_l4_bytes(1025) == 1280 * 16
+    assert L.rtn_out_tcp4_bytes(1025) == 1280 * 8
     assert L.rtn_out_addr6_bytes(1) == CF * 32
     assert L.rtn_out_dlv_bytes(64, 2) == CF * 2 * 8      # masks only: the frame is the rank in dlv_bitmap
     assert L.rtn_out_bitmap_bytes(0xFFFFFFFF) == ((1 << 32) // 64) * 8   # 64-bit arithmetic, no wrap
-    assert L.rtn_out_l4_bytes(0xFFFFFFFF) == (1 << 32) * 24
+    assert L.rtn_out_l4_bytes(0xFFFFFFFF) == (1 << 32) * 16
 
 
 def test_headers_are_c(tmp_path):
@@ -144,7 +145,8 @@ _RUST_C = {"u8": "uint8_t", "u16": "uint16_t", "u32": "uint32_t", "u64": "uint64
            "usize": "size_t"}
 _RUST_TO_HEADER = {"RtnBatch": "rtn_batch_t", "RtnPcOut": "rtn_pc_out_t", "RtnL4Ctx": "rtn_l4ctx_t",
                    "RtnConn": "rtn_conn_t", "RtnProgramInfo": "rtn_program_info_t",
-                   "RtnFlowItem": "rtn_flow_item_t", "RtnFlowRule": "rtn_flow_rule_t"}
+                   "RtnFlowItem": "rtn_flow_item_t", "RtnFlowRule": "rtn_flow_rule_t",
+                   "RtnStageSlab": "rtn_stage_slab_t"}
 
 
 def _c_decl(t: str, f: str) -> str:
@@ -180,7 +182,7 @@ def test_integration_rust_structs_match_header(tmp_path):
     text = (Path(__file__).resolve().parent.parent / "INTEGRATION.md").read_text()
     structs = _rust_structs(text)
     assert set(_RUST_TO_HEADER) <= set(structs), sorted(structs)
-    src = '#include "retina_pc.h"\n#include "retina_hw.h"\n#include <stddef.h>\n#include <stdint.h>\n'
+    src = '#include "retina_pc.h"\n#include "retina_hw.h"\n#include "retina_stage.h"\n#include <stddef.h>\n#include <stdint.h>\n'
     for name, cname in _RUST_TO_HEADER.items():
         src += f"typedef struct {{\n"
         for f, t in structs[name]:
@@ -199,7 +201,7 @@ def test_integration_rust_structs_match_header(tmp_path):
     # every field of the C structs is in the twin (no field missing at the end either)
     import re
 
-    hdr = (inc / "retina_pc.h").read_text() + (inc / "retina_hw.h").read_text()
+    hdr = (inc / "retina_pc.h").read_text() + (inc / "retina_hw.h").read_text() + (inc / "retina_stage.h").read_text()
     for name, cname in _RUST_TO_HEADER.items():
         body = re.search(r"typedef struct \w+ \{([^{}]*)\} " + cname + ";", hdr).group(1)
         cfields = re.findall(r"^\s*[\w\s\*]+?\b(\w+)(?:\[\w+\])?;", re.sub(r"/\*.*?\*/", "", body, flags=re.S), re.M)

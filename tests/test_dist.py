@@ -43,7 +43,9 @@ def _rank_main(rank: int, world: int, port: int, cfg: str, q) -> None:
                                int((r["dm"] != 0).any(1).sum()) if r["dm"].size else 0], dtype=torch.int64)
         times = torch.tensor([0.5 + rank, 1.0 * rank], dtype=torch.float64)
         rdist.reduce_totals(totals, times)
-        q.put((rank, totals.tolist(), times.tolist()))
+        rows = rdist.gather_rows([float(rank), 2.0 * rank + 0.5])  # bench.py's per-rank report
+        rdist.host_barrier()  # where bench.py parks the ranks during rank 0's CPU baseline
+        q.put((rank, totals.tolist(), times.tolist(), rows.tolist()))
     finally:
         dist.destroy_process_group()
 
@@ -72,9 +74,10 @@ def test_two_rank_shards_reduce_to_single_process(cfg):
     r = helpers.oracle_run(SETS[cfg], slab, stride, dlen)
     exp = [N_PER_RANK * world, int(r["pc"].sum()), int(r["fwd"].sum()),
            int((r["dm"] != 0).any(1).sum()) if r["dm"].size else 0]
-    for rank, totals, times in got:
+    for rank, totals, times, rows in got:
         assert totals == exp, (rank, totals, exp)
         assert times == [0.5 + world - 1, 1.0 * (world - 1)]
+        assert rows == [[float(r), 2.0 * r + 0.5] for r in range(world)]
     assert rdist.aggregate_mpps(N_PER_RANK, world, 10, 1.0) == N_PER_RANK * world * 10 / 1e6
 
 

@@ -43,7 +43,8 @@ def nostores(src: str) -> str:
     src = _sub(src, "    if (d) {", "    if (d && a.n == 0u) {")
     src = _sub(src, "  const bool six = fwd && v.v6 && (a.flags & 1u);", "  const bool six = false;")
     src = _sub(src, "    rtn_flush<CONN>(a, ring, cring, ch, lane, ch.nrec - ch.nflushed);", "")
-    src = _sub(src, "  if (ch.nrec - ch.nflushed >= RTN_FLUSH) {", "  if (false) {")
+    src = _sub(src, "    if (ch.ntcp != ch.ntflushed) rtn_flush_t4(a, ring4, ch, lane, ch.ntcp - ch.ntflushed);", "")
+    src = _sub(src, "  if (fr || ft) {", "  if (false) {")
     return src
 
 
@@ -53,10 +54,10 @@ VARIANTS = {"base": base, "ceiling": ceiling, "nostores": nostores}
 def dense(src: str) -> str:
     """Timing only: a chunk's records go to one dense 128-record region (chunk * 128 + k, no block
     interleave; chunks with more than 128 records overlap their neighbours)."""
-    src = _sub(src, "rtn_v4u* dst = reinterpret_cast<rtn_v4u*>(a.recs + rtn_rec_slot(nch, ch.rec_base / (64u * RTN_CHUNK_GROUPS), ch.nflushed));",
-               "rtn_v4u* dst = reinterpret_cast<rtn_v4u*>(a.recs + ch.rec_base / 4u + ch.nflushed);")
-    return _sub(src, "if (k < nv4) RTN_ST(dst + (k / (RTN_RB * 3u / 2u)) * nch * (RTN_RB * 3u / 2u) + k % (RTN_RB * 3u / 2u), src[k]);",
-                "if (k < nv4) RTN_ST(dst + k, src[k]);")
+    src = _sub(src, "rtn_v4u* dst = reinterpret_cast<rtn_v4u*>(a.recs + rtn_rec_slot(nch, c, ch.nflushed));",
+               "rtn_v4u* dst = reinterpret_cast<rtn_v4u*>(a.recs + ch.rec_base / 2u + ch.nflushed);")
+    return _sub(src, "if (lane < nl) RTN_ST(dst + (lane / RTN_RB) * nch * RTN_RB + lane % RTN_RB, src[lane]);",
+                "if (lane < nl) RTN_ST(dst + lane, src[lane]);")
 
 
 def nobitmaps(src: str) -> str:
@@ -144,7 +145,7 @@ def rb128(src: str) -> str:
 def wpb2(src: str) -> str:
     """Per-block LDS sized for 2 waves (run with RTN_BLOCK=128: 128-thread blocks, one chunk per
     wave as before, so a block retires after 2 chunks instead of 4)."""
-    for arr in ("rtn_ring[4]", "rtn_cring[4]", "rtn_ring6[4]", "rtn_tile[4]"):
+    for arr in ("rtn_ring[4]", "rtn_ring4[4]", "rtn_cring[4]", "rtn_ring6[4]", "rtn_tile[4]"):
         src = _sub(src, arr, arr.replace("[4]", "[2]"))
     return src
 
