@@ -332,7 +332,7 @@ def e2e_rate(ctx, slab: np.ndarray, dlen: np.ndarray, stride: int, dev, chunk: i
 
 
 def e2e_from_mbufs(ctx, slab: np.ndarray, dlen: np.ndarray, stride: int, dev, frames: int = 1 << 21,
-                   chunk: int = 1 << 19, nstreams: int = 4, threads: int | None = None) -> dict:
+                   chunk: int = 1 << 18, nstreams: int = 2, threads: int | None = None) -> dict:
     """End-to-end rate from DPDK-shaped mbufs (include/retina_stage.h): `frames` frames, each in
     its own 2176-B buffer (128-B headroom) of a host mbuf pool, handed over in shuffled order as
     an array of data pointers (buf_addr + data_off) + data_len, as rx_burst leaves them
@@ -340,7 +340,10 @@ def e2e_from_mbufs(ctx, slab: np.ndarray, dlen: np.ndarray, stride: int, dev, fr
     `nstreams` streams, with the kernel writing its records straight into pinned host memory
     and the bitmaps copied back (as e2e_rate):
       host   -- rtn_stage_mbufs on pinned host threads into pinned staging buffers, H2D, kernel;
-      gpu    -- rtn_stage_gather: the GPU reads the mbufs from the registered pool, kernel."""
+      gpu    -- rtn_stage_gather: the GPU reads the mbufs from the registered pool, kernel;
+      hybrid -- both at once on disjoint parts of every chunk (the GPU pull is bound by the host's
+                read-request rate, the host form by its copy threads: they add up until the link
+                is full); the GPU's share is the best of a few fractions."""
     import torch
 
     from retina_amd import pc
@@ -355,6 +358,7 @@ def e2e_from_mbufs(ctx, slab: np.ndarray, dlen: np.ndarray, stride: int, dev, fr
     h_ptrs = torch.from_numpy(ptrs.view(np.int64)).pin_memory()
     h_dl = torch.from_numpy(dl.view(np.int16)).pin_memory()
     streams = [torch.cuda.Stream(dev) for _ in range(nstreams)]
+    gstreams = [torch.cuda.Stream(dev) for _ in range(nstreams)]  # hybrid: the GPU-pulled parts
     rows_cap = pc.gather_ext_rows(chunk)
     sets = []
     for _ in range(nstreams):
@@ -376,6 +380,16 @@ def e2e_from_mbufs(ctx, slab: np.ndarray, dlen: np.ndarray, stride: int, dev, fr
             "s_chunk": torch.empty(chunk // 256, dtype=torch.int32).pin_memory(),
             "s_dl": torch.empty(chunk, dtype=torch.int16).pin_memory(),
             "done": None,
+            # hybrid: the GPU-pulled part's device buffers and outputs, on a second stream
+            "head2": torch.empty(chunk * 64, dtype=torch.uint8, device=dev),
+            "ext2": torch.empty(rows_cap * 64, dtype=torch.uint8, device=dev),
+            "chunk2": torch.empty(chunk // 256, dtype=torch.int32, device=dev),
+            "dl2": torch.empty(chunk, dtype=torch.int16, device=dev),
+            "out2": dataclasses.replace(zc2 := ctx.alloc_outputs(chunk, addr6=True, counters=False),
+                                        l4=pc.MappedHost(torch.empty(zc2.l4.numel(), dtype=torch.uint8).pin_memory()),
+                                        addr6=pc.MappedHost(torch.empty(zc2.addr6.numel(), dtype=torch.uint8).pin_memory()),
+                                        tcp4=pc.MappedHost(torch.empty(zc2.tcp4.numel(), dtype=torch.uint8).pin_memory())),
+            "h_bm2": torch.empty(out.pc_bitmap.numel() * 2, dtype=torch.uint8).pin_memory(),
         })
     plan = [(s, min(chunk, m - s)) for s in range(0, m, chunk)]
 
@@ -401,7 +415,10 @@ def e2e_from_mbufs(ctx, slab: np.ndarray, dlen: np.ndarray, stride: int, dev, fr
     q = _host_cpus()["cgroup_quota_cpus"]
     if q:
         cpus = cpus[:max(1, int(q))]
-    nthr = threads if threads is not None else max(1, len(cpus) - 2)  # leave the submitting thread a core
+    # leave cores to the submitting thread and the HIP runtime: with every core of a CPU quota
+    # busy copying, the quota throttles the thread that feeds the copy engine (tools/e2e_probe.py:
+    # 12 of 16 ran faster than 14)
+    nthr = threads if threads is not None else max(1, min(12, len(cpus) - 4))
     stager = pc.Stager(nthr, cpus[-nthr:] if len(cpus) >= nthr else None)
     staged = {}
 
@@ -433,6 +450,37 @@ def e2e_from_mbufs(ctx, slab: np.ndarray, dlen: np.ndarray, stride: int, dev, fr
                 b["done"] = ev
                 finish(k, st, b, nfr)
 
+    def hybrid_pass(frac: float):
+        for k, (s, nfr) in enumerate(plan):
+            st, sg, b = streams[k % nstreams], gstreams[k % nstreams], sets[k % nstreams]
+            g = int(nfr * frac) // 256 * 256
+            if b["done"] is not None:
+                b["done"].synchronize()
+            if g:  # the GPU pulls frames [s, s + g) while the host threads stage the rest
+                with torch.cuda.stream(sg):
+                    mp.gather(h_ptrs[s:s + g], h_dl[s:s + g], g, b["head2"], b["ext2"], b["chunk2"], b["dl2"], stream=sg)
+                    ctx.run(b["head2"], 64, b["dl2"], g, b["out2"], stream=sg, ext=b["ext2"], ext_chunk=b["chunk2"])
+                    nb = b["out2"].pc_bitmap.numel()
+                    b["h_bm2"][:nb].copy_(b["out2"].pc_bitmap, non_blocking=True)
+                    b["h_bm2"][nb:].copy_(b["out2"].fwd_bitmap, non_blocking=True)
+            h = nfr - g
+            rows, mx = stage(k, s + g, h, b)
+            with torch.cuda.stream(st):
+                b["head"][:h * 64].copy_(b["s_head"][:h * 64], non_blocking=True)
+                b["dl"][:h].copy_(b["s_dl"][:h], non_blocking=True)
+                if mx <= 64:
+                    ctx.run(b["head"], 64, b["dl"], h, b["out"], stream=st, dl_le64=True)
+                else:
+                    if rows:
+                        b["ext"][:rows * 64].copy_(b["s_ext"][:rows * 64], non_blocking=True)
+                    b["chunk"][:(h + 255) // 256].copy_(b["s_chunk"][:(h + 255) // 256], non_blocking=True)
+                    ctx.run(b["head"], 64, b["dl"], h, b["out"], stream=st, ext=b["ext"][:max(rows, 1) * 64],
+                            ext_chunk=b["chunk"])
+                ev = torch.cuda.Event()
+                ev.record(st)
+                b["done"] = ev
+                finish(k, st, b, h)
+
     def stage_only():
         for k, (s, nfr) in enumerate(plan):
             stage(k, s, nfr, sets[k % nstreams])
@@ -459,6 +507,9 @@ def e2e_from_mbufs(ctx, slab: np.ndarray, dlen: np.ndarray, stride: int, dev, fr
     res["host"]["stage_only_mpps"] = round(m / timed(stage_only) / 1e6, 1)
     rows = sum(r for r, mx in staged.values() if mx > 64)  # ext rows copied (none when every frame fits 64 B)
     res["host"]["h2d_bytes_per_frame"] = round((m * (64 + 2) + rows * 64) / m, 2)
+    hy = {f: round(m / timed(lambda: hybrid_pass(f)) / 1e6, 1) for f in (0.25, 0.35, 0.45)}
+    best = max(hy, key=hy.get)
+    res["hybrid"] = {"mpps": hy[best], "gpu_share": best, "by_share": {str(f): v for f, v in hy.items()}}
     win = max(res, key=lambda k: res[k]["mpps"])
     del stager, mp
     return {"frames": m, "chunk_frames": chunk, "streams": nstreams, "pool_bytes": int(pool.nbytes),
@@ -466,7 +517,8 @@ def e2e_from_mbufs(ctx, slab: np.ndarray, dlen: np.ndarray, stride: int, dev, fr
             "mpps": res[win]["mpps"],
             "note": "mbuf-shaped buffers (2176 B, 128-B headroom, shuffled), data pointers + data_len as "
                     "rx_burst leaves them; host = rtn_stage_mbufs threads into pinned buffers + H2D; "
-                    "gpu = rtn_stage_gather reading the hipHostRegister'd pool over PCIe; both then rtn_pc_run "
+                    "gpu = rtn_stage_gather reading the hipHostRegister'd pool over PCIe; hybrid = both on disjoint "
+                    "parts of each chunk; all then rtn_pc_run "
                     "with records written into pinned host memory and the bitmaps copied back"}
 
 

@@ -144,6 +144,10 @@ __device__ __forceinline__ void rtn_ct_wave_sync() {
 __device__ __forceinline__ bool rtn_ct_occupied(const rtn_u32* occ, rtn_u32 slot) {
   return (occ[slot >> 5] >> (slot & 31u)) & 1u;
 }
+// the same at device scope, for the insert pass, which sets bits while it reads them
+__device__ __forceinline__ bool rtn_ct_occupied_now(rtn_u32* occ, rtn_u32 slot) {
+  return (__hip_atomic_load(&occ[slot >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> (slot & 31u)) & 1u;
+}
 
 __device__ __forceinline__ rtn_u64* rtn_ct_tag(const rtn_ct_args& a, rtn_u32 slot) {
   return reinterpret_cast<rtn_u64*>(a.table + (rtn_u64)slot * 16u);
@@ -206,8 +210,11 @@ __device__ __forceinline__ rtn_u64 rtn_ct_rslot(const rtn_ct_chunk& ch, rtn_u32 
   return ((rtn_u64)(k >> 6) * ch.nch + ch.c) * 64u + (k & 63u);
 }
 
+// lane l's 64-bit value (readlane returns int: go through u32, or the low half sign-extends)
 __device__ __forceinline__ rtn_u64 rtn_ct_rl64(rtn_u64 v, int l) {
-  return (rtn_u64)__builtin_amdgcn_readlane((rtn_u32)v, l) | ((rtn_u64)__builtin_amdgcn_readlane((rtn_u32)(v >> 32), l) << 32);
+  const rtn_u32 lo = (rtn_u32)__builtin_amdgcn_readlane((int)(rtn_u32)v, l);
+  const rtn_u32 hi = (rtn_u32)__builtin_amdgcn_readlane((int)(rtn_u32)(v >> 32), l);
+  return (rtn_u64)lo | ((rtn_u64)hi << 32);
 }
 
 // The chunk's bitmap words and the rtn_conn_t of its records: cv[j] / has[j] for record
@@ -342,13 +349,17 @@ extern "C" __global__ void __launch_bounds__(64u * RTN_CT_CPB) rtn_ct_insert(rtn
     for (rtn_u32 p = 0; p < RTN_CT_MAXPROBE; ++p) {
       bool more = false;
       if (active && !at_empty) {
-        const rtn_u64 t = rtn_ct_occupied(a.occ, slot)
+        // occupancy, tag and epoch are read at device scope (through to L2): slots are claimed
+        // during this launch, by other blocks and by this wave's earlier rounds, and a copy of the
+        // line in this CU's L1 would show a claimed slot as empty
+        const rtn_u64 t = rtn_ct_occupied_now(a.occ, slot)
                               ? __hip_atomic_load(rtn_ct_tag(a, slot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                               : RTN_CT_EMPTY;
         if (t == k.fp) {
           // `first` only matters for a slot opened in this batch (epoch == this batch, or 0 while
           // its claimer is still writing it); an older connection's frames are plain hits
-          const rtn_u32 ep = a.table[(rtn_u64)slot * 16u + 2u];
+          const rtn_u32 ep = __hip_atomic_load(&a.table[(rtn_u64)slot * 16u + 2u], __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
           if (ep == 0u || ep == a.epoch) atomicMin(&a.table[(rtn_u64)slot * 16u + 3u], frame);
           active = false;
         } else if (t == RTN_CT_EMPTY) {

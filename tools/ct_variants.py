@@ -15,7 +15,15 @@ def base(src: str) -> str:
     return src
 
 
-VARIANTS = {"base": base}
+def dbg(src: str) -> str:
+    """printf every insert-pass opener whose frame index is past the batch (debugging)."""
+    return _sub(src, "      frame = rtn_ct_frame(ch, it.k);\n",
+                "      frame = rtn_ct_frame(ch, it.k);\n"
+                "      if (frame >= a.n) printf(\"BADFRAME c=%u lane=%u rd=%u e=%u nop=%u k=%u frame=%u total=%u p=%u,%u,%u w=%llx,%llx,%llx,%llx cv=%llx\\n\", "
+                "c, lane, rd, e, nop, it.k, frame, ch.total, ch.p0, ch.p01, ch.p012, ch.w[0], ch.w[1], ch.w[2], ch.w[3], it.cv);\n")
+
+
+VARIANTS = {"base": base, "dbg": dbg}
 
 
 def write(name: str, outdir: Path) -> Path:
