@@ -68,7 +68,9 @@ int32_t rtn_ct_destroy(rtn_ct_t* ct);
 /* One batch (n frames, the same batch rtn_pc_run processed into `pc`): two launches on `stream`.
  * out: device array of rtn_out_ct_bytes(n) bytes, indexed like the records. */
 int32_t rtn_ct_process(rtn_ct_t* ct, const rtn_pc_out_t* pc, uint32_t n, rtn_ct_entry_t* out, void* stream);
-/* Remove connections (device array of slot handles); their slots become tombstones. */
+/* Remove connections (device array of slot handles); their slots become tombstones, except that a
+   run of tombstones followed by an empty slot becomes empty again (it ends no probe chain). A slot
+   listed twice is removed once. */
 int32_t rtn_ct_remove(rtn_ct_t* ct, const uint32_t* slots, uint32_t n, void* stream);
 /* Compact tombstones away: every live connection moves; new_slot (device, capacity entries)
  * receives old slot -> new slot (RTN_CT_NO_SLOT for dead ones). Synchronous. */

@@ -534,20 +534,38 @@ extern "C" __global__ void __launch_bounds__(64u * RTN_CT_CPB) rtn_ct_lookup(rtn
   }
 }
 
-extern "C" __global__ void __launch_bounds__(256) rtn_ct_remove_k(rtn_u32* table, rtn_u32* live, const rtn_u32* slots,
-                                                                 rtn_u32 n, rtn_u32 cap_mask) {
+extern "C" __global__ void __launch_bounds__(256) rtn_ct_remove_k(rtn_u32* table, rtn_u32* occ, rtn_u32* live,
+                                                                 const rtn_u32* slots, rtn_u32 n, rtn_u32 cap_mask) {
   const rtn_u32 i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const rtn_u32 slot = slots[i] & cap_mask;
   rtn_u64* tag = reinterpret_cast<rtn_u64*>(table + (rtn_u64)slot * 16u);
-  const rtn_u64 t = *tag;
-  if (t > RTN_CT_REMOVED) {
-    // a tombstone: lookups walk past it, an insert reuses it (epoch 0 and first 0xffffffff: the
-    // state of a slot whose claimer has not written it yet)
-    table[(rtn_u64)slot * 16u + 2u] = 0u;
-    table[(rtn_u64)slot * 16u + 3u] = 0xffffffffu;
-    *tag = RTN_CT_REMOVED;
-    atomicSub(&live[0], 1u);
+  const rtn_u64 t = __hip_atomic_load(tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (t <= RTN_CT_REMOVED) return;
+  // a tombstone: lookups walk past it, an insert reuses it (epoch 0 and first 0xffffffff: the
+  // state of a slot whose claimer has not written it yet). The CAS makes a slot listed twice
+  // count once.
+  table[(rtn_u64)slot * 16u + 2u] = 0u;
+  table[(rtn_u64)slot * 16u + 3u] = 0xffffffffu;
+  if (atomicCAS(tag, t, RTN_CT_REMOVED) != t) return;
+  atomicSub(&live[0], 1u);
+  // A tombstone followed by an empty slot ends no probe chain (every chain through it would have
+  // stopped at that empty slot), so it becomes empty again, and so does the run of tombstones
+  // before it. Without this, keys whose home slot is empty keep consuming empty slots while
+  // tombstones pile up elsewhere, until no chain reaches an empty slot (FULL) before a rebuild.
+  // Two removals racing on neighbours: each publishes its own write, fences, then reads the
+  // other's slot, so at least one of them sees both tombstones and clears the pair. No insert or
+  // lookup runs during this launch, so an empty slot stays empty throughout.
+  __threadfence();
+  rtn_u32 s = slot;
+  for (rtn_u32 p = 0; p < cap_mask; ++p) {
+    const rtn_u32 nx = (s + 1u) & cap_mask;
+    if ((__hip_atomic_load(&occ[nx >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> (nx & 31u)) & 1u) break;
+    rtn_u64* ts = reinterpret_cast<rtn_u64*>(table + (rtn_u64)s * 16u);
+    if (atomicCAS(ts, RTN_CT_REMOVED, RTN_CT_EMPTY) != RTN_CT_REMOVED) break;
+    atomicAnd(&occ[s >> 5], ~(1u << (s & 31u)));
+    __threadfence();
+    s = (s - 1u) & cap_mask;
   }
 }
 

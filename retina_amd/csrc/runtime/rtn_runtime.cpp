@@ -952,8 +952,9 @@ int32_t rtn_ct_remove(rtn_ct_t* ct, const uint32_t* slots, uint32_t n, void* str
   if (n == 0) return RTN_OK;
   uint32_t mask = ct->cap - 1u;
   uint32_t* table = ct->table;
+  uint32_t* occ = ct->occ;
   uint32_t* live = ct->live;
-  void* p[] = {&table, &live, &slots, &n, &mask};
+  void* p[] = {&table, &occ, &live, &slots, &n, &mask};
   hipError_t e = hipModuleLaunchKernel(ct->remove, (n + 255u) / 256u, 1, 1, 256, 1, 1, 0,
                                        reinterpret_cast<hipStream_t>(stream), p, nullptr);
   return e == hipSuccess ? RTN_OK : hip_fail("rtn_ct_remove", e);

@@ -87,5 +87,47 @@ def main() -> None:
         print(f"   after removal: counter {r.ct.stats()['live']} model {len(model.present)}", flush=True)
 
 
-if __name__ == "__main__":
+if __name__ == "__main__" and len(sys.argv) == 1:
     main()
+
+
+def churn() -> None:
+    """tests/test_ct.py::test_ct_churn_reuses_removed_slots, printing the table around any FULL."""
+    import torch
+
+    torch.cuda.init()
+    import test_ct as T
+    import helpers
+    from oracle import conn as oconn
+    from retina_amd import pc
+
+    pc.lib().rtn_ct_table.restype = C.c_void_p
+    rng = np.random.default_rng(23)
+    r = T._Run(cap_log2=10, max_conn=900)
+    model = oconn.TableModel(max_connections=900)
+    ids, owner = {}, {}
+    for b in range(14):
+        pool = helpers.flow_pool(rng, 300)
+        frames = helpers.flow_frames(rng, pool, 900, p_syn=0.9)
+        exp = model.process(T._model_frames(frames, r.pf))
+        got = r.batch(frames)
+        tab = table_host(r.ct, r.ct.capacity)
+        tags = tab[:, 0].astype(np.uint64) | (tab[:, 1].astype(np.uint64) << 32)
+        print(f"batch {b}: live {r.ct.stats()['live']} empty {(tags == 0).sum()} removed {(tags == 1).sum()} "
+              f"used {(tags > 1).sum()} FULL {int((got[:, 1] & 0xFF == pc.CT_FULL).sum())}", flush=True)
+        if (got[:, 1] & 0xFF == pc.CT_FULL).any():
+            bad = np.nonzero(got[:, 1] & 0xFF == pc.CT_FULL)[0][:3]
+            for i in bad:
+                print("   FULL frame", int(i), "model", exp[i], flush=True)
+            break
+        T._check(got, exp, ids, owner)
+        live = list(model.present.items())
+        slots = np.array([ids[mid] for _, (mid, _) in live], np.uint32)
+        r.ct.remove(r.torch.from_numpy(slots.view(np.int32)).to("cuda:0"))
+        model.remove([k for k, _ in live])
+        for _, (mid, _) in live:
+            owner.pop(ids.pop(mid), None)
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "churn":
+    churn()
