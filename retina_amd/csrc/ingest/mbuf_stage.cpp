@@ -90,15 +90,13 @@ struct rtn_stager {
 
 namespace {
 
-// 64 bytes into a head slot or ext row: plain copy, or (experiments build, RTN_STAGE_NT) streaming
-// stores that skip the read-for-ownership of the destination line.
-#ifdef RTN_EXPERIMENTS
-const bool kStageNt = getenv("RTN_STAGE_NT") != nullptr;
-#else
-constexpr bool kStageNt = false;
-#endif
+// 64 bytes into a head slot or ext row. Streaming stores when the slab is 64-B aligned: a head
+// slot or ext row is written whole and read next by the DMA engine, so the plain copy's
+// read-for-ownership of the destination line is pure waste (cfg2, 14 threads: 608 -> 1047 Mpkt/s,
+// profiles/r3a_stage_probe_*). Each worker fences its own streaming stores before it reports done.
+template <bool NT>
 inline void copy64(uint8_t* dst, const uint8_t* src) {
-  if (kStageNt) {
+  if (NT) {
     const __m128i* s = reinterpret_cast<const __m128i*>(src);
     __m128i* d = reinterpret_cast<__m128i*>(dst);
     const __m128i a = _mm_loadu_si128(s), b = _mm_loadu_si128(s + 1), c = _mm_loadu_si128(s + 2),
@@ -113,6 +111,7 @@ inline void copy64(uint8_t* dst, const uint8_t* src) {
 }
 
 // Pass 1 over frames [f0, f1) (whole chunks): head slots, data_len, need bits, rows per chunk.
+template <bool NT>
 void stage_heads(const uint8_t* const* data, const uint16_t* dl, uint32_t f0, uint32_t f1,
                  const rtn_stage_slab_t& s, uint64_t* need, uint32_t* chunk_rows, uint16_t& dl_max) {
   uint16_t mx = 0;
@@ -122,7 +121,7 @@ void stage_heads(const uint8_t* const* data, const uint16_t* dl, uint32_t f0, ui
     if (i + kPrefetch < f1) __builtin_prefetch(data[i + kPrefetch]);
     const uint8_t* src = data[i];
     uint8_t* h = s.head + (uint64_t)i * 64u;
-    copy64(h, src);
+    copy64<NT>(h, src);
     const uint16_t d = dl[i];
     s.data_len[i] = d;
     mx = d > mx ? d : mx;
@@ -132,9 +131,11 @@ void stage_heads(const uint8_t* const* data, const uint16_t* dl, uint32_t f0, ui
     }
   }
   dl_max = mx;
+  if (NT) _mm_sfence();
 }
 
 // Pass 2: ext rows of the needing frames of [f0, f1), from ext_chunk (already the prefix).
+template <bool NT>
 void stage_ext(const uint8_t* const* data, uint32_t f0, uint32_t f1, const rtn_stage_slab_t& s,
                const uint64_t* need) {
   for (uint32_t c = f0 / RTN_CHUNK_FRAMES; c * RTN_CHUNK_FRAMES < f1; ++c) {
@@ -152,12 +153,29 @@ void stage_ext(const uint8_t* const* data, uint32_t f0, uint32_t f1, const rtn_s
       }
       while (b) {
         const uint32_t i = w * 64u + (uint32_t)__builtin_ctzll(b);
-        copy64(s.ext + row * 64u, data[i] + 64);
+        copy64<NT>(s.ext + row * 64u, data[i] + 64);
         ++row;
         b &= b - 1u;
       }
     }
   }
+  if (NT) _mm_sfence();
+}
+
+void stage_heads_any(bool nt, const uint8_t* const* data, const uint16_t* dl, uint32_t f0, uint32_t f1,
+                     const rtn_stage_slab_t& s, uint64_t* need, uint32_t* chunk_rows, uint16_t& dl_max) {
+  if (nt)
+    stage_heads<true>(data, dl, f0, f1, s, need, chunk_rows, dl_max);
+  else
+    stage_heads<false>(data, dl, f0, f1, s, need, chunk_rows, dl_max);
+}
+
+void stage_ext_any(bool nt, const uint8_t* const* data, uint32_t f0, uint32_t f1, const rtn_stage_slab_t& s,
+                   const uint64_t* need) {
+  if (nt)
+    stage_ext<true>(data, f0, f1, s, need);
+  else
+    stage_ext<false>(data, f0, f1, s, need);
 }
 
 }  // namespace
@@ -208,20 +226,21 @@ int32_t rtn_stage_mbufs(rtn_stager_t* st, const uint8_t* const* data, const uint
   const rtn_stage_slab_t s = *slab;
   uint64_t* need = st->need.data();
   uint32_t* crow = st->chunk_rows.data();
+  // streaming stores need 16-B-aligned destinations; slabs from pinned allocators are page aligned
+  const bool nt = (((uintptr_t)s.head | (uintptr_t)s.ext) & 63u) == 0;
   const uint32_t T = (n < kInlineFrames || st->workers.empty()) ? 1u
                      : std::min<uint32_t>((uint32_t)st->workers.size(), nch);
   st->dl_max.assign(T, 0);
   // slice t: chunks [nch * t / T, nch * (t + 1) / T)
   auto lo = [&](uint32_t t) { return std::min<uint64_t>((uint64_t)nch * t / T * RTN_CHUNK_FRAMES, n); };
   if (T == 1) {
-    stage_heads(data, data_len, 0, n, s, need, crow, st->dl_max[0]);
+    stage_heads_any(nt, data, data_len, 0, n, s, need, crow, st->dl_max[0]);
   } else {
     st->job = [&](uint32_t k) {
-      if (k < T) stage_heads(data, data_len, (uint32_t)lo(k), (uint32_t)lo(k + 1), s, need, crow, st->dl_max[k]);
+      if (k < T) stage_heads_any(nt, data, data_len, (uint32_t)lo(k), (uint32_t)lo(k + 1), s, need, crow, st->dl_max[k]);
     };
     st->run_all();
   }
-  if (kStageNt) _mm_sfence();
   uint64_t r = 0;
   for (uint32_t c = 0; c < nch; ++c) {
     s.ext_chunk[c] = (uint32_t)r;
@@ -234,15 +253,14 @@ int32_t rtn_stage_mbufs(rtn_stager_t* st, const uint8_t* const* data, const uint
   if (r && !s.ext) return fail(RTN_EINVAL, "ext rows needed but slab->ext is null");
   if (r) {
     if (T == 1) {
-      stage_ext(data, 0, n, s, need);
+      stage_ext_any(nt, data, 0, n, s, need);
     } else {
       st->job = [&](uint32_t k) {
-        if (k < T) stage_ext(data, (uint32_t)lo(k), (uint32_t)lo(k + 1), s, need);
+        if (k < T) stage_ext_any(nt, data, (uint32_t)lo(k), (uint32_t)lo(k + 1), s, need);
       };
       st->run_all();
     }
   }
-  if (kStageNt) _mm_sfence();
   *rows = (uint32_t)r;
   return RTN_OK;
 }

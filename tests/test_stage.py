@@ -45,9 +45,17 @@ def expected(slab, dlen, stride):
     return head, ext[:rows * 64], chunk
 
 
-def host_stage(stager, ptrs, dlen, n, ext_cap=None):
-    head = np.zeros(max(n, 1) * 64, np.uint8)
-    ext = np.zeros(max(n if ext_cap is None else ext_cap, 1) * 64, np.uint8)
+def _buf(nbytes: int, off: int) -> np.ndarray:
+    """nbytes zero bytes starting `off` bytes past a 64-B boundary (0: the streaming-store copy;
+    otherwise the plain one)."""
+    raw = np.zeros(nbytes + 128, np.uint8)
+    a = (-raw.ctypes.data) % 64 + off
+    return raw[a:a + nbytes]
+
+
+def host_stage(stager, ptrs, dlen, n, ext_cap=None, off=0):
+    head = _buf(max(n, 1) * 64, off)
+    ext = _buf(max(n if ext_cap is None else ext_cap, 1) * 64, off)
     chunk = np.zeros(max((n + 255) // 256, 1), np.uint32)
     dl = np.zeros(max(n, 1), np.uint16)
     rows, mx = stager.stage(ptrs, dlen, head, ext, chunk, dl, n=n, ext_cap=ext_cap)
@@ -70,6 +78,17 @@ def test_host_stage_matches_packer(name, n, threads):
     assert np.array_equal(chunk, ec)
     assert np.array_equal(head, eh)
     assert np.array_equal(ext, ee)
+
+
+@pytest.mark.parametrize("off", [0, 16, 1])
+def test_host_stage_slab_alignment(off):
+    """Aligned slabs take streaming stores, others a plain copy: same bytes either way."""
+    slab, dlen, stride, _ = corpus("cfg3", 9000)
+    n = len(dlen)
+    pool, ptrs = pc.mbuf_pool(slab, dlen, stride, seed=3)
+    head, ext, chunk, dl, rows, mx = host_stage(pc.Stager(4), ptrs, dlen, n, off=off)
+    eh, ee, ec = expected(slab, dlen, stride)
+    assert np.array_equal(head, eh) and np.array_equal(ext, ee) and np.array_equal(chunk, ec)
 
 
 def test_host_stage_empty_and_errors():

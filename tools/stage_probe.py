@@ -24,8 +24,6 @@ def main() -> None:
     import bench
     from retina_amd import pc
 
-    if os.environ.get("RTN_STAGE_NT"):  # streaming stores: the experiments build only
-        pc._LIB_PATH = pc._LIB_PATH.with_name("libretina_pc_exp.so")
     cfg = sys.argv[1] if len(sys.argv) > 1 else "cfg2"
     m = int(sys.argv[2]) if len(sys.argv) > 2 else 1 << 21
     stride = bench.CONFIGS[cfg][1]
@@ -51,7 +49,7 @@ def main() -> None:
         if t > len(cpus):
             continue
         st = pc.Stager(t, cpus[-t:])
-        print(json.dumps({"cfg": cfg, "threads": t, "nt": bool(os.environ.get("RTN_STAGE_NT")),
+        print(json.dumps({"cfg": cfg, "threads": t, "nt": True,
                           "stage_mpps": round(rate(st), 1)}), flush=True)
     # with a concurrent DMA stream (1 GiB pinned -> HBM, back to back)
     dev = torch.device("cuda", 0)

@@ -209,6 +209,22 @@ def withconn(src: str) -> str:
 VARIANTS.update({"withconn": withconn})
 
 
+def not4(src: str) -> str:
+    """Timing only: no IPv4-TCP seq/ack side stream (the tcp4 ring and its stores)."""
+    return _sub(src, "const bool t4 = fwd && v.v4 && v.tcp && (a.flags & 32u);", "const bool t4 = false;")
+
+
+def pad64(src: str) -> str:
+    """Chunk-end stores padded to 64 B (the HBM write request size, TCC_EA0_WRREQ_64B) instead of
+    whole 128-B lines: records to 4, seq/ack entries to 8, IPv6 address records to 2."""
+    src = _sub(src, "  const rtn_u32 nl = (nrecs + 7u) & ~7u;", "  const rtn_u32 nl = (nrecs + 3u) & ~3u;")
+    src = _sub(src, "  const rtn_u32 nl = ((nent + 1u) / 2u + 7u) & ~7u;", "  const rtn_u32 nl = ((nent + 1u) / 2u + 3u) & ~3u;")
+    return _sub(src, "  const rtn_u32 nv4 = ((nent + 3u) & ~3u) * 2u;", "  const rtn_u32 nv4 = ((nent + 1u) & ~1u) * 2u;")
+
+
+VARIANTS.update({"not4": not4, "pad64": pad64})
+
+
 def write(name: str, outdir: Path) -> Path:
     """A variant file: a '+'-joined list of VARIANTS applied to the current kernel, or
     'file=<path>' (a kernel source as is, e.g. an older revision: git show REV:path > file)."""
