@@ -223,6 +223,26 @@ __device__ __forceinline__ void rtn_extract_v(const rtn_u32 (&w)[NW], bool q, rt
   for (int j = 0; j < 5; ++j) v.l4w[j] = rtn_alignbyte2(s0[j + 1], s0[j]);
 }
 
+// Per-lane offsets from the four common stacks only: L3 at 14 or 18 (802.1Q) and L4 right after
+// an IPv4 header without options or the IPv6 fixed header, so the L4 window starts at word
+// 8 + q + 5 * v6. Every candidate view word is one alignbyte of two neighbours, then two selects
+// (q, then v6) pick a lane's: 41 VALU against the barrel shifter's 81 (cfg3 / cfg4 mix all four
+// in every wave).
+template <int NW>
+__device__ __forceinline__ void rtn_extract_q6(const rtn_u32 (&w)[NW], bool q, bool six, rtn_view& v) {
+  const rtn_u32 mq = rtn_mask(q), m6 = rtn_mask(six);
+  rtn_u32 x[16];  // x[i] = the view word at byte 4 * (i + 3) + 2
+#pragma unroll
+  for (int i = 0; i < 16; ++i) x[i] = rtn_alignbyte2(rtn_w(w, i + 4), rtn_w(w, i + 3));
+#pragma unroll
+  for (int j = 0; j < 10; ++j) v.l3w[j] = rtn_sel(mq, x[j + 1], x[j]);
+  rtn_u32 y[10];  // the L4 window of a lane without IPv6 (word 8 + q), then 5 words further
+#pragma unroll
+  for (int i = 0; i < 10; ++i) y[i] = rtn_sel(mq, x[i + 6], x[i + 5]);
+#pragma unroll
+  for (int j = 0; j < 5; ++j) v.l4w[j] = rtn_sel(m6, y[j + 5], y[j]);
+}
+
 // Parse one slot held in registers (w = its first 64 * NW/16 bytes).
 template <int NW>
 __device__ __forceinline__ void rtn_parse(const rtn_u32 (&w)[NW], rtn_u32 dl, rtn_view& v) {
@@ -264,6 +284,8 @@ __device__ __forceinline__ void rtn_parse(const rtn_u32 (&w)[NW], rtn_u32 dl, rt
     rtn_extract_c<NW, 14, 54>(w, v);         // Eth / IPv6
   } else if (uni && ukey == (18u | (58u << 8))) {
     rtn_extract_c<NW, 18, 58>(w, v);         // Eth / 802.1Q / IPv6
+  } else if (__ballot(ip && v.l4off != v.l3off + (v.v6 ? 40u : 20u)) == 0ull) {  // (802.1ad is never IP here)
+    rtn_extract_q6<NW>(w, q, v.v6, v);     // {Eth, 802.1Q} x {IPv4 (IHL 5), IPv6}, per lane
   } else {
     rtn_extract_v<NW>(w, q, v.l4off, v);
   }
@@ -386,9 +408,11 @@ __device__ __forceinline__ void rtn_flush(const rtn_args& a, const rtn_u64* ring
     rtn_v4u* cdst = reinterpret_cast<rtn_v4u*>(a.conn + rtn_rec_slot(nch, c, ch.nflushed));
     if (lane < nc) RTN_ST(cdst + (lane / (RTN_RB / 2u)) * nch * (RTN_RB / 2u) + lane % (RTN_RB / 2u), csrc[lane]);
   }
-  // whole 128-B lines only (8 records): the block starts line-aligned and the tail is padded with
-  // stale ring bytes into the chunk's unused record space (a partial line costs a read-modify-write)
-  const rtn_u32 nl = (nrecs + 7u) & ~7u;
+  // whole 64-B write requests only (4 records; TCC_EA0_WRREQ_64B is the memory-side write size): the
+  // block starts line-aligned and the tail is padded with stale ring bytes into the chunk's unused
+  // record space (a partial request costs a read-modify-write; padding to 128-B lines instead
+  // writes 32 B more per stream and chunk on average: cfg4 +1 %, tools/variants.py pad64)
+  const rtn_u32 nl = (nrecs + 3u) & ~3u;
   const rtn_v4u* src = reinterpret_cast<const rtn_v4u*>(ring) + (ch.nflushed & (RTN_RING - 1u));
   rtn_v4u* dst = reinterpret_cast<rtn_v4u*>(a.recs + rtn_rec_slot(nch, c, ch.nflushed));
   // (a block of RTN_RB records is RTN_RB lanes; a flush may span several blocks)
@@ -396,11 +420,11 @@ __device__ __forceinline__ void rtn_flush(const rtn_args& a, const rtn_u64* ring
 }
 
 // seq/ack entries of IPv4 TCP records [ntflushed, ntflushed + nent): 8 B each, two per lane,
-// whole 128-B lines, 64-entry blocks at RTN_REC_INDEX of the chunk's IPv4-TCP rank.
+// whole 64-B requests, 64-entry blocks at RTN_REC_INDEX of the chunk's IPv4-TCP rank.
 __device__ __forceinline__ void rtn_flush_t4(const rtn_args& a, const rtn_u64* ring4, const rtn_chunk& ch,
                                              rtn_u32 lane, rtn_u32 nent) {
   const rtn_u64 nch = rtn_nchunks(a.n);
-  const rtn_u32 nl = ((nent + 1u) / 2u + 7u) & ~7u;
+  const rtn_u32 nl = ((nent + 1u) / 2u + 3u) & ~3u;
   const rtn_v4u* src = reinterpret_cast<const rtn_v4u*>(ring4 + (ch.ntflushed & (RTN_RING - 1u)));
   rtn_v4u* dst = reinterpret_cast<rtn_v4u*>(a.tcp4 + rtn_rec_slot(nch, ch.rec_base / (64u * RTN_CHUNK_GROUPS), ch.ntflushed));
   if (lane < nl) RTN_ST(dst + (lane / (RTN_RB / 2u)) * nch * (RTN_RB / 2u) + lane % (RTN_RB / 2u), src[lane]);
@@ -418,12 +442,12 @@ __device__ __forceinline__ void rtn_flush_t4(const rtn_args& a, const rtn_u64* r
 #define RTN_FLUSH6 32u
 
 // Stores ring entries [nv6flushed, nv6flushed + nent) (nent <= RTN_RING6), rounded up to whole
-// 128-B lines (4 entries): a partial line costs a read-modify-write. Only a chunk's last store is
+// 64-B write requests (2 entries): a partial request costs a read-modify-write. Only a chunk's last store is
 // partial, and its padding (stale ring bytes) lands in the chunk's unused addr6 space, as for the
 // record blocks.
 __device__ __forceinline__ void rtn_flush6(const rtn_args& a, const rtn_v4u* ring6, const rtn_chunk& ch, rtn_u32 lane,
                                            rtn_u32 nent) {
-  const rtn_u32 nv4 = ((nent + 3u) & ~3u) * 2u;  // 16-B halves
+  const rtn_u32 nv4 = ((nent + 1u) & ~1u) * 2u;  // 16-B halves
   rtn_v4u* dst = reinterpret_cast<rtn_v4u*>(a.addr6 + (ch.rec_base + ch.nv6flushed) * 32u);
 #pragma unroll
   for (rtn_u32 j = 0; j < 2u; ++j) {

@@ -45,12 +45,13 @@ def main() -> None:
             st.stage(ptrs, dlen, head, ext, chunk, dl, n=m, cap=m, ext_cap=m)
         return m * reps / (time.perf_counter() - t0) / 1e6
 
-    for t in (1, 4, 8, 14, 16):
+    for t in (1, 4, 8, 12, 14, 16):
         if t > len(cpus):
             continue
-        st = pc.Stager(t, cpus[-t:])
-        print(json.dumps({"cfg": cfg, "threads": t, "nt": True,
-                          "stage_mpps": round(rate(st), 1)}), flush=True)
+        pinned = rate(pc.Stager(t, cpus[-t:]))
+        free = rate(pc.Stager(t, None))  # left to the scheduler (any CPU of the affinity mask)
+        print(json.dumps({"cfg": cfg, "threads": t, "nt": True, "stage_mpps": round(pinned, 1),
+                          "stage_mpps_unpinned": round(free, 1)}), flush=True)
     # with a concurrent DMA stream (1 GiB pinned -> HBM, back to back)
     dev = torch.device("cuda", 0)
     src = torch.empty(1 << 30, dtype=torch.uint8).pin_memory()
