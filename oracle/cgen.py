@@ -298,9 +298,11 @@ class OracleLib:
                              rec.ctypes.data, dm.ctypes.data)
         return {"pc": pc.astype(bool), "fwd": fwd.astype(bool), "l4": rec, "dm": dm[:, :self.nd]}
 
-    def bench(self, frame_ptrs: np.ndarray, dlen: np.ndarray, reps: int, cpus: list[int]) -> np.ndarray:
+    def bench(self, frame_ptrs: np.ndarray, dlen: np.ndarray, reps: int, cpus: list[int], pin: bool = True) -> np.ndarray:
+        """len(cpus) threads on disjoint shards, each pinned to its CPU, or (pin=False) left to the
+        scheduler."""
         out = np.zeros(4, np.uint64)
         cp = np.asarray(cpus, np.int32)
-        self.lib.oracle_bench(frame_ptrs.ctypes.data, dlen.ctypes.data, len(dlen), reps, len(cpus), cp.ctypes.data,
-                              out.ctypes.data)
+        self.lib.oracle_bench(frame_ptrs.ctypes.data, dlen.ctypes.data, len(dlen), reps, len(cpus),
+                              cp.ctypes.data if pin else None, out.ctypes.data)
         return out

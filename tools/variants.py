@@ -230,7 +230,23 @@ def noq6(src: str) -> str:
                 "  } else if (false) {")
 
 
-VARIANTS.update({"not4": not4, "pad128": pad128, "noq6": noq6})
+def t4dense(src: str) -> str:
+    """Timing only: a chunk's seq/ack entries dense per chunk (chunk * 256 + IPv4-TCP rank, like
+    addr6) instead of in RTN_REC_INDEX blocks: one contiguous run per chunk."""
+    return _sub(src, "  if (lane < nl) RTN_ST(dst + (lane / (RTN_RB / 2u)) * nch * (RTN_RB / 2u) + lane % (RTN_RB / 2u), src[lane]);\n}\n\n// IPv6",
+                "  (void)dst;\n  rtn_v4u* dd = reinterpret_cast<rtn_v4u*>(a.tcp4 + ch.rec_base + ch.ntflushed);\n"
+                "  if (lane < nl) RTN_ST(dd + lane, src[lane]);\n}\n\n// IPv6")
+
+
+def recdense(src: str) -> str:
+    """Timing only: a chunk's records dense per chunk (chunk * 256 + rank) instead of in
+    RTN_REC_INDEX blocks (the connection-stage entries stay interleaved)."""
+    return _sub(src, "  if (lane < nl) RTN_ST(dst + (lane / RTN_RB) * nch * RTN_RB + lane % RTN_RB, src[lane]);",
+                "  (void)dst;\n  rtn_v4u* dd = reinterpret_cast<rtn_v4u*>(a.recs + ch.rec_base + ch.nflushed);\n"
+                "  if (lane < nl) RTN_ST(dd + lane, src[lane]);")
+
+
+VARIANTS.update({"not4": not4, "pad128": pad128, "noq6": noq6, "t4dense": t4dense, "recdense": recdense})
 
 
 def write(name: str, outdir: Path) -> Path:
