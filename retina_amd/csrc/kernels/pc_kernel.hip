@@ -441,6 +441,10 @@ __device__ __forceinline__ void rtn_flush_t4(const rtn_args& a, const rtn_u64* r
 #define RTN_RING6 96u
 #define RTN_FLUSH6 32u
 
+// Ring slot of position x < 2 * RTN_RING6 (a wave-uniform base below RTN_RING6 plus a lane's rank
+// below 64): one subtract and a min instead of the modulo's quarter-rate multiplies.
+__device__ __forceinline__ rtn_u32 rtn_ring6_at(rtn_u32 x) { return min(x, x - RTN_RING6); }
+
 // Stores ring entries [nv6flushed, nv6flushed + nent) (nent <= RTN_RING6), rounded up to whole
 // 64-B write requests (2 entries): a partial request costs a read-modify-write. Only a chunk's last store is
 // partial, and its padding (stale ring bytes) lands in the chunk's unused addr6 space, as for the
@@ -452,7 +456,7 @@ __device__ __forceinline__ void rtn_flush6(const rtn_args& a, const rtn_v4u* rin
 #pragma unroll
   for (rtn_u32 j = 0; j < 2u; ++j) {
     const rtn_u32 k = lane + 64u * j;
-    if (k < nv4) RTN_ST(dst + k, ring6[((ch.nv6flushed + k / 2u) % RTN_RING6) * 2u + (k & 1u)]);
+    if (k < nv4) RTN_ST(dst + k, ring6[rtn_ring6_at(ch.nv6flushed % RTN_RING6 + k / 2u) * 2u + (k & 1u)]);
   }
 }
 
@@ -585,8 +589,9 @@ __device__ __forceinline__ void rtn_group(const rtn_args& a, rtn_u32 g, rtn_u32 
     // Fewer than RTN_FLUSH6 entries are pending when a group starts (every whole block is stored
     // below), so the group's at most 64 entries always find free slots in the 96-entry ring.
     if (six) {
-      ring6[(r6 % RTN_RING6) * 2u] = s0;
-      ring6[(r6 % RTN_RING6) * 2u + 1u] = s1;
+      const rtn_u32 at = rtn_ring6_at(ch.nv6 % RTN_RING6 + rank6);
+      ring6[at * 2u] = s0;
+      ring6[at * 2u + 1u] = s1;
     }
     ch.nv6 += cnt6;
     if (ch.nv6 - ch.nv6flushed >= RTN_FLUSH6) {  // every whole block pending (at most 64 entries)

@@ -246,7 +246,31 @@ def recdense(src: str) -> str:
                 "  if (lane < nl) RTN_ST(dd + lane, src[lane]);")
 
 
-VARIANTS.update({"not4": not4, "pad128": pad128, "noq6": noq6, "t4dense": t4dense, "recdense": recdense})
+def dmsb(src: str) -> str:
+    """A scheduling barrier after every statement-mask bit of the generated filter: the compiler
+    cannot hoist later predicates' compares above it (their lane masks stay out of SGPRs until
+    needed)."""
+    src = _sub(src, "#define RTN_DM_SET(m, w, b, r) ((m)[w] |= (r) ? (1ull << (b)) : 0ull)",
+               "#define RTN_DM_SET(m, w, b, r) do { (m)[w] |= (r) ? (1ull << (b)) : 0ull; __builtin_amdgcn_sched_barrier(0); } while (0)")
+    return _sub(src, "#define RTN_DM_SETV(m, w, b, r) ((m)[w] |= (r) ? (1ull << (b)) : 0ull)",
+                "#define RTN_DM_SETV(m, w, b, r) do { (m)[w] |= (r) ? (1ull << (b)) : 0ull; __builtin_amdgcn_sched_barrier(0); } while (0)")
+
+
+def ksb(src: str) -> str:
+    """A scheduling barrier at every predicate constant of the generated filter: predicates are
+    evaluated in program order."""
+    return _sub(src, "#ifndef RTN_K\n", "#define RTN_K(c) (__builtin_amdgcn_sched_barrier(0), (c))\n#ifndef RTN_K\n")
+
+
+def ring6mod(src: str) -> str:
+    """The IPv6 ring indexed with a modulo (the round-2 form) instead of rtn_ring6_at."""
+    src = _sub(src, "ring6[rtn_ring6_at(ch.nv6flushed % RTN_RING6 + k / 2u) * 2u + (k & 1u)]",
+               "ring6[((ch.nv6flushed + k / 2u) % RTN_RING6) * 2u + (k & 1u)]")
+    return _sub(src, "const rtn_u32 at = rtn_ring6_at(ch.nv6 % RTN_RING6 + rank6);", "const rtn_u32 at = (ch.nv6 + rank6) % RTN_RING6;")
+
+
+VARIANTS.update({"not4": not4, "pad128": pad128, "noq6": noq6, "t4dense": t4dense, "recdense": recdense,
+                 "dmsb": dmsb, "ksb": ksb, "ring6mod": ring6mod})
 
 
 def write(name: str, outdir: Path) -> Path:
