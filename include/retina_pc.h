@@ -176,9 +176,9 @@ typedef struct rtn_pc_out {
   uint64_t* fwd_bitmap;  /* [ceil(n/64)]  ... and L4Context::new succeeded (goes to conntrack) */
   rtn_l4ctx_t* l4;       /* [ceil(n/256)*256] (rtn_out_l4_bytes) at RTN_REC_INDEX; unused slots undefined */
   uint8_t* addr6;        /* optional [ceil(n/256)*256][32] (rtn_out_addr6_bytes): src|dst of the IPv6
-                          records; a chunk's last store is padded to whole 128-B lines, so it may
-                          write up to 3 entries past the chunk's last IPv6 record (inside the
-                          chunk's 256 entries)                                              */
+                          records; a chunk's last store is padded to whole 64-B write requests,
+                          so it may write 1 entry past the chunk's last IPv6 record (inside
+                          the chunk's 256 entries)                                          */
   uint64_t* dlv_bitmap;  /* [ceil(n/64)] frames with >= 1 packet-level callback (if any)     */
   uint64_t* dlv_records; /* [ceil(n/256)*256][deliver_words]: statement mask; the frame is the
                           record's rank among its chunk's dlv_bitmap bits (as for l4)        */

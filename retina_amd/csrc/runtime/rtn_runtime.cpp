@@ -179,8 +179,25 @@ uint64_t fnv1a(const std::string& s) {
 std::mutex g_cache_mu;
 std::map<uint64_t, std::shared_ptr<std::vector<uint8_t>>> g_cache;  // source hash -> code object
 
+// Extra hiprtc options, experiments build only: RTN_KERNEL_OPTS="-mllvm -x ..." (space-separated),
+// so tools/ab.py can time compiler settings against each other in one process.
+std::vector<std::string> env_opts() {
+  std::vector<std::string> o;
+#ifdef RTN_EXPERIMENTS
+  if (const char* e = getenv("RTN_KERNEL_OPTS")) {
+    std::stringstream ss(e);
+    std::string t;
+    while (ss >> t) o.push_back(t);
+  }
+#endif
+  return o;
+}
+
 int32_t compile_code_object(const std::string& src, std::shared_ptr<std::vector<uint8_t>>& out) {
-  const uint64_t h = fnv1a(src);
+  const std::vector<std::string> extra = env_opts();
+  std::string key = src;
+  for (const auto& e : extra) key += "\n//opt " + e;
+  const uint64_t h = fnv1a(key);
   {
     std::lock_guard<std::mutex> lk(g_cache_mu);
     auto it = g_cache.find(h);
@@ -194,8 +211,9 @@ int32_t compile_code_object(const std::string& src, std::shared_ptr<std::vector<
     return fail(RTN_ECOMPILE, "hiprtcCreateProgram failed");
   std::string arch = "--offload-arch=gfx950";
   if (const char* a = getenv("RTN_OFFLOAD_ARCH")) arch = std::string("--offload-arch=") + a;
-  const char* opts[] = {arch.c_str(), "-O3", "-std=c++17"};
-  hiprtcResult r = hiprtcCompileProgram(prog, 3, opts);
+  std::vector<const char*> opts = {arch.c_str(), "-O3", "-std=c++17"};
+  for (const auto& e : extra) opts.push_back(e.c_str());
+  hiprtcResult r = hiprtcCompileProgram(prog, (int)opts.size(), opts.data());
   size_t ls = 0;
   hiprtcGetProgramLogSize(prog, &ls);
   std::string log(ls, '\0');

@@ -251,8 +251,8 @@ def test_large_tree_uses_nested_form_and_matches(gpu):
 
 
 def test_misaligned_record_array_is_einval(gpu):
-    """l4 / addr6 / conn take 16-B-per-lane stores: a misaligned array is refused (RTN_EINVAL)
-    before anything is launched, and the same context still runs on aligned outputs."""
+    """l4 / addr6 / conn / tcp4 take 16-B-per-lane stores: a misaligned array is refused
+    (RTN_EINVAL) before anything is launched, and the same context still runs on aligned outputs."""
     import dataclasses
 
     import torch
@@ -262,7 +262,7 @@ def test_misaligned_record_array_is_einval(gpu):
     d_slab = torch.from_numpy(slab).cuda()
     d_dlen = torch.from_numpy(dlen.view(np.int16)).cuda()
     out = ctx.alloc_outputs(len(dlen), conn=True)
-    for field in ("l4", "addr6", "conn"):
+    for field in ("l4", "addr6", "conn", "tcp4"):
         t = getattr(out, field)
         bad = dataclasses.replace(out, **{field: torch.empty(t.numel() + 16, dtype=torch.uint8, device="cuda")[8:]})
         with pytest.raises(pc.RetinaError) as e:

@@ -1,6 +1,6 @@
 """In-process A/B timing of kernel variants on one GPU (tools/README.md).
 
-    python tools/ab.py cfg2|cfg3|cfg4 VARIANT[:DEFINES][@GRID][^CPW][#split|#compact|#mono] ... [--reps R]
+    python tools/ab.py cfg2|cfg3|cfg4 VARIANT[:DEFINES][@GRID][%OPTS][^CPW][#split|#compact|#mono] ... [--reps R]
         [--frames N] [--mono] [--compact]
 
 VARIANT names a tools/variants.py function (or several joined with '+'). Prints, per entry, the
@@ -78,6 +78,8 @@ def main() -> None:
             os.environ["RTN_CPW"] = cpw
         else:
             os.environ.pop("RTN_CPW", None)
+        name, _, kopts = name.partition("%")  # VARIANT%opt,opt: extra hiprtc options (comma-separated)
+        os.environ["RTN_KERNEL_OPTS"] = kopts.replace(",", " ")
         name, _, grid = name.partition("@")
         name, _, defs = name.partition(":")
         os.environ["RTN_KERNEL_TEMPLATE"] = str(variants.write(name, tmp))

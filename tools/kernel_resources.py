@@ -69,12 +69,14 @@ def main() -> None:
     spec = bench.spec_for(args.cfg)
     tmp = Path(tempfile.mkdtemp())
     for v in args.variants or ["base"]:
-        os.environ["RTN_KERNEL_TEMPLATE"] = str(variants.write(v, tmp))
+        name, _, kopts = v.partition("%")  # VARIANT%opt,opt: extra hiprtc options, as in tools/ab.py
+        os.environ["RTN_KERNEL_OPTS"] = kopts.replace(",", " ")
+        os.environ["RTN_KERNEL_TEMPLATE"] = str(variants.write(name, tmp))
         co = pc.Program.from_spec(spec).code_object()
         isa = None
         if args.isa:
             args.isa.mkdir(parents=True, exist_ok=True)
-            isa = args.isa / f"{args.cfg}_{v.replace('+', '_')}.s"
+            isa = args.isa / f"{args.cfg}_{name.replace('+', '_')}{'_' + str(abs(hash(kopts)) % 10**6) if kopts else ''}.s"
         for r in report(co, isa):
             if r["kernel"].startswith("rtn_pc_kernel"):
                 print(f"{args.cfg} {v:24s} {r['kernel']:22s} vgpr {r['vgpr']:3d} ({r['waves_per_simd']} waves) "

@@ -273,6 +273,21 @@ VARIANTS.update({"not4": not4, "pad128": pad128, "noq6": noq6, "t4dense": t4dens
                  "dmsb": dmsb, "ksb": ksb, "ring6mod": ring6mod})
 
 
+def nodlv(src: str) -> str:
+    """Timing only: no delivery-record stores (the dlv bitmap is still written)."""
+    return _sub(src, "    if (d) {\n      const rtn_u64 slot_i", "    if (d && a.n == 0u) {\n      const rtn_u64 slot_i")
+
+
+def dlvnt(src: str) -> str:
+    """Delivery records stored non-temporally instead of through the caches (8-B stores at the
+    record's rank)."""
+    return _sub(src, "      for (int j = 0; j < RTN_DELIVER_WORDS; ++j) RTN_ST8(dp + j, dm[j]);",
+                "      for (int j = 0; j < RTN_DELIVER_WORDS; ++j) __builtin_nontemporal_store(dm[j], dp + j);")
+
+
+VARIANTS.update({"nodlv": nodlv, "dlvnt": dlvnt})
+
+
 def write(name: str, outdir: Path) -> Path:
     """A variant file: a '+'-joined list of VARIANTS applied to the current kernel, or
     'file=<path>' (a kernel source as is, e.g. an older revision: git show REV:path > file)."""
