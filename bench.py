@@ -268,13 +268,13 @@ def e2e_rate(ctx, slab: np.ndarray, dlen: np.ndarray, stride: int, dev, chunk: i
                      torch.empty(chunk // pc.CHUNK_FRAMES + 1, dtype=torch.int32, device=dev),
                      ctx.alloc_outputs(chunk, addr6=wide, counters=False)))
     h_out = [torch.empty(bufs[0][4].l4.numel(), dtype=torch.uint8).pin_memory() for _ in range(nstreams)]
-    h_t4 = [torch.empty(bufs[0][4].tcp4.numel(), dtype=torch.uint8).pin_memory() for _ in range(nstreams)]
+    h_t4 = [torch.empty(bufs[0][4].seqack.numel(), dtype=torch.uint8).pin_memory() for _ in range(nstreams)]
     h_bm = [torch.empty(bufs[0][4].pc_bitmap.numel() * 2, dtype=torch.uint8).pin_memory() for _ in range(nstreams)]
     h_a6 = [torch.empty(bufs[0][4].addr6.numel(), dtype=torch.uint8).pin_memory() for _ in range(nstreams)] if wide else None
 
     # zero-copy outputs: the kernel writes records (and IPv6 addresses) straight into pinned host
     # memory over PCIe, so only what was produced crosses the link (pc.MappedHost)
-    zc_outs = [dataclasses.replace(bufs[k][4], l4=pc.MappedHost(h_out[k]), tcp4=pc.MappedHost(h_t4[k]),
+    zc_outs = [dataclasses.replace(bufs[k][4], l4=pc.MappedHost(h_out[k]), seqack=pc.MappedHost(h_t4[k]),
                                    addr6=pc.MappedHost(h_a6[k]) if wide else None) for k in range(nstreams)]
 
     def one_pass(zero_copy: bool = True):
@@ -295,7 +295,7 @@ def e2e_rate(ctx, slab: np.ndarray, dlen: np.ndarray, stride: int, dev, chunk: i
                     ctx.run(d_slab, run_stride, d_dlen, m, out, stream=st, dl_le64=dl_le64)
                 if not zero_copy:
                     h_out[k % nstreams].copy_(out.l4, non_blocking=True)
-                    h_t4[k % nstreams].copy_(out.tcp4, non_blocking=True)
+                    h_t4[k % nstreams].copy_(out.seqack, non_blocking=True)
                     if wide:
                         h_a6[k % nstreams].copy_(out.addr6, non_blocking=True)
                 nb = out.pc_bitmap.numel()
@@ -373,8 +373,8 @@ def e2e_from_mbufs(ctx, slab: np.ndarray, dlen: np.ndarray, stride: int, dev, fr
         out = ctx.alloc_outputs(chunk, addr6=True, counters=False)
         h_l4 = torch.empty(out.l4.numel(), dtype=torch.uint8).pin_memory()
         h_a6 = torch.empty(out.addr6.numel(), dtype=torch.uint8).pin_memory()
-        h_t4 = torch.empty(out.tcp4.numel(), dtype=torch.uint8).pin_memory()
-        zc = dataclasses.replace(out, l4=pc.MappedHost(h_l4), addr6=pc.MappedHost(h_a6), tcp4=pc.MappedHost(h_t4))
+        h_t4 = torch.empty(out.seqack.numel(), dtype=torch.uint8).pin_memory()
+        zc = dataclasses.replace(out, l4=pc.MappedHost(h_l4), addr6=pc.MappedHost(h_a6), seqack=pc.MappedHost(h_t4))
         sets.append({
             "head": torch.empty(chunk * 64, dtype=torch.uint8, device=dev),
             "ext": torch.empty(rows_cap * 64, dtype=torch.uint8, device=dev),
@@ -396,7 +396,7 @@ def e2e_from_mbufs(ctx, slab: np.ndarray, dlen: np.ndarray, stride: int, dev, fr
             "out2": dataclasses.replace(zc2 := ctx.alloc_outputs(chunk, addr6=True, counters=False),
                                         l4=pc.MappedHost(torch.empty(zc2.l4.numel(), dtype=torch.uint8).pin_memory()),
                                         addr6=pc.MappedHost(torch.empty(zc2.addr6.numel(), dtype=torch.uint8).pin_memory()),
-                                        tcp4=pc.MappedHost(torch.empty(zc2.tcp4.numel(), dtype=torch.uint8).pin_memory())),
+                                        seqack=pc.MappedHost(torch.empty(zc2.seqack.numel(), dtype=torch.uint8).pin_memory())),
             "h_bm2": torch.empty(out.pc_bitmap.numel() * 2, dtype=torch.uint8).pin_memory(),
         })
     plan = [(s, min(chunk, m - s)) for s in range(0, m, chunk)]

@@ -115,12 +115,16 @@ void walk(const HostSet& h, bool with_ct, Totals& t, FILE* dump) {
         }
         if (dump) {
           char src[40], dst[40];
-          if (v6) {
-            const uint8_t* a = h.addr6 + k6 * 32u;
+          if (v6) {  // source bytes 0..7 in the record (w0, w1), the other 24 B in addr6
+            const uint8_t* a = h.addr6 + k6 * 24u;
+            uint8_t s0[8];
+            std::memcpy(s0, &r.w0, 4);
+            std::memcpy(s0 + 4, &r.w1, 4);
             char* p = src;
-            for (int j = 0; j < 16; ++j) p += sprintf(p, "%02x", a[j]);
+            for (int j = 0; j < 8; ++j) p += sprintf(p, "%02x", s0[j]);
+            for (int j = 0; j < 8; ++j) p += sprintf(p, "%02x", a[j]);
             p = dst;
-            for (int j = 16; j < 32; ++j) p += sprintf(p, "%02x", a[j]);
+            for (int j = 8; j < 24; ++j) p += sprintf(p, "%02x", a[j]);
           } else {
             sprintf(src, "%08x", r.w0);  // an IPv4 record's addresses
             sprintf(dst, "%08x", r.w1);

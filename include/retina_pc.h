@@ -51,10 +51,11 @@ typedef struct rtn_pc rtn_pc_t;           /* program loaded on one device, ready
 /* Compacted L4Context of a forwarded packet (PacketContinue && L4Context::new Ok), 16 bytes.
  * Together with its side streams it holds every field of conntrack/pdu.rs:66-84, and no field
  * that is always zero for the record's kind:
- *   IPv4 TCP: w0 = src, w1 = dst (u32::from(Ipv4Addr), host order); seq_no | ack_no << 32 in tcp4
+ *   IPv4 TCP: w0 = src, w1 = dst (u32::from(Ipv4Addr), host order); seq_no | ack_no << 32 in seqack
  *   IPv4 UDP: w0 = src, w1 = dst                                       (seq_no = ack_no = 0)
- *   IPv6 TCP: w0 = seq_no, w1 = ack_no; src | dst in addr6
- *   IPv6 UDP: w0 = w1 = 0;              src | dst in addr6             (seq_no = ack_no = 0)
+ *   IPv6 TCP: w0|w1 = src bytes 0..7 (memory order); src bytes 8..15 | dst in addr6 (24 B);
+ *             seq_no | ack_no << 32 in seqack
+ *   IPv6 UDP: w0|w1 = src bytes 0..7; src bytes 8..15 | dst in addr6   (seq_no = ack_no = 0)
  * The frame a record belongs to is implied by its position (see rtn_pc_out_t). */
 typedef struct rtn_l4ctx {
   uint32_t w0;
@@ -67,12 +68,12 @@ typedef struct rtn_l4ctx {
  * stored as offset >> 2 in 6 bits. */
 #define RTN_L4_OFFSET(m) ((((m) & 0x3Fu) << 2) | 2u)            /* L4Context.offset           */
 #define RTN_L4_PROTO(m) (((m) & 0x40u) ? 17u : 6u)                 /* L4Context.proto            */
-#define RTN_L4_IPV6(m) (((m) >> 7) & 1u)                           /* src/dst are IPv6 (addr6)   */
+#define RTN_L4_IPV6(m) (((m) >> 7) & 1u)                           /* IPv6 (w0|w1 + addr6)       */
 #define RTN_L4_FLAGS(m) (((m) >> 8) & 0xFFu)                       /* L4Context.flags (TCP)      */
 #define RTN_L4_LENGTH(m) ((m) >> 16)                               /* L4Context.length           */
-/* seq_no | ack_no << 32 of an IPv4 TCP record, in rtn_pc_out_t.tcp4 */
-#define RTN_TCP4_SEQ(t) ((uint32_t)(t))
-#define RTN_TCP4_ACK(t) ((uint32_t)((t) >> 32))
+/* seq_no | ack_no << 32 of a TCP record, in rtn_pc_out_t.seqack */
+#define RTN_SEQACK_SEQ(t) ((uint32_t)(t))
+#define RTN_SEQACK_ACK(t) ((uint32_t)((t) >> 32))
 
 /* Connection stage of a forwarded frame (8 bytes, indexed like its rtn_l4ctx_t):
  *   hash  = rtn_conn_hash of the canonical ConnId: MurmurHash3-x86-32 block + finaliser steps,
@@ -161,24 +162,24 @@ static inline int rtn_ext_needed(const uint8_t* head, uint16_t data_len) {
  * in blocks of RTN_REC_BLOCK, block j of chunk c at block slot j * nchunks + c, so the chunks'
  * first blocks form one dense stream, their second blocks the next, and so on (the stores of a
  * partly-forwarded batch stay dense).
- * The j-th forwarded IPv6 frame of chunk c (records with RTN_L4_IPV6) has its addresses at
- * addr6[c * RTN_CHUNK_FRAMES + j]; dlv_records are ranked by dlv_bitmap the same way (dense per
- * chunk). The j-th IPv4 TCP record of chunk c (neither RTN_L4_IPV6 nor UDP) has its seq/ack at
- * tcp4[RTN_REC_INDEX(n, c, j)]. Bitmaps hold bit i % 64 of word i / 64. */
+ * The j-th forwarded IPv6 frame of chunk c (records with RTN_L4_IPV6) has the rest of its
+ * addresses (source bytes 8..15, destination) at addr6[c * RTN_CHUNK_FRAMES + j]; dlv_records are
+ * ranked by dlv_bitmap the same way (dense per chunk). The j-th TCP record of chunk c (not UDP)
+ * has its seq/ack at seqack[RTN_REC_INDEX(n, c, j)]. Bitmaps hold bit i % 64 of word i / 64. */
 #define RTN_CHUNK_FRAMES 256u
 #define RTN_REC_BLOCK 64u
 #define RTN_REC_INDEX(n, chunk, k)                                                             \
   (((uint64_t)((k) / RTN_REC_BLOCK) * (((uint64_t)(n) + RTN_CHUNK_FRAMES - 1u) / RTN_CHUNK_FRAMES) + \
     (uint64_t)(chunk)) * RTN_REC_BLOCK + (uint64_t)((k) % RTN_REC_BLOCK))
-/* l4, addr6, conn and tcp4 must be 16-byte aligned (RTN_EINVAL otherwise). */
+/* l4, addr6, conn and seqack must be 16-byte aligned (RTN_EINVAL otherwise). */
 typedef struct rtn_pc_out {
   uint64_t* pc_bitmap;   /* [ceil(n/64)]  Actions.data contains PacketContinue               */
   uint64_t* fwd_bitmap;  /* [ceil(n/64)]  ... and L4Context::new succeeded (goes to conntrack) */
   rtn_l4ctx_t* l4;       /* [ceil(n/256)*256] (rtn_out_l4_bytes) at RTN_REC_INDEX; unused slots undefined */
-  uint8_t* addr6;        /* optional [ceil(n/256)*256][32] (rtn_out_addr6_bytes): src|dst of the IPv6
-                          records; a chunk's last store is padded to whole 64-B write requests,
-                          so it may write 1 entry past the chunk's last IPv6 record (inside
-                          the chunk's 256 entries)                                          */
+  uint8_t* addr6;        /* optional [ceil(n/256)*256][24] (rtn_out_addr6_bytes): source bytes 8..15
+                          and destination of the IPv6 records (raw); a chunk's last store is
+                          padded to whole 64-B write requests, so it may write up to 2 entries
+                          past the chunk's last IPv6 record (inside the chunk's 256 entries) */
   uint64_t* dlv_bitmap;  /* [ceil(n/64)] frames with >= 1 packet-level callback (if any)     */
   uint64_t* dlv_records; /* [ceil(n/256)*256][deliver_words]: statement mask; the frame is the
                           record's rank among its chunk's dlv_bitmap bits (as for l4)        */
@@ -187,8 +188,8 @@ typedef struct rtn_pc_out {
   rtn_conn_t* conn;      /* optional [ceil(n/256)*256]: connection stage, indexed like l4       */
   uint64_t* conn_dlv;    /* [ceil(n/256)*256][conn_words] first-packet statement masks; required
                           with conn when the program has first-packet statements           */
-  uint64_t* tcp4;        /* optional [ceil(n/256)*256] (rtn_out_tcp4_bytes): seq_no | ack_no << 32
-                          of the IPv4 TCP records (NULL: not written)                       */
+  uint64_t* seqack;      /* optional [ceil(n/256)*256] (rtn_out_seqack_bytes): seq_no | ack_no << 32
+                          of the TCP records, IPv4 and IPv6 (NULL: not written)             */
 } rtn_pc_out_t;
 
 /* The counters block (u32 word offsets; the byte sums are u64 over two words). The stats names
@@ -304,7 +305,7 @@ size_t rtn_out_addr6_bytes(uint32_t n);
 size_t rtn_out_dlv_bytes(uint32_t n, uint32_t deliver_words);
 size_t rtn_out_conn_bytes(uint32_t n);
 size_t rtn_out_conn_dlv_bytes(uint32_t n, uint32_t conn_words);
-size_t rtn_out_tcp4_bytes(uint32_t n);
+size_t rtn_out_seqack_bytes(uint32_t n);
 
 #ifdef __cplusplus
 }

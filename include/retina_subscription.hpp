@@ -116,7 +116,7 @@ class Burst {
   void process_packets(F&& f) const {
     const size_t nch = (n_ + RTN_CHUNK_FRAMES - 1) / RTN_CHUNK_FRAMES;
     for (size_t c = 0; c < nch; ++c) {
-      uint32_t k = 0, k6 = 0, k4 = 0;  // records, IPv6 records, IPv4 TCP records of chunk c
+      uint32_t k = 0, k6 = 0, kt = 0;  // records, IPv6 records, TCP records of chunk c
       for (size_t i = c * RTN_CHUNK_FRAMES; i < n_ && i < (c + 1) * RTN_CHUNK_FRAMES; ++i) {
         if (!bit(fwd_, i)) continue;
         const rtn_l4ctx_t& r = l4_[RTN_REC_INDEX(n_, c, k)];
@@ -128,27 +128,25 @@ class Burst {
         x.src.port = (uint16_t)(r.ports & 0xFFFFu);
         x.dst.port = (uint16_t)(r.ports >> 16);
         const bool tcp = x.proto == 6;
-        if (RTN_L4_IPV6(r.meta)) {
-          const uint8_t* a = &addr6_[(c * RTN_CHUNK_FRAMES + k6) * 32u];
+        if (RTN_L4_IPV6(r.meta)) {  // source bytes 0..7 in the record, the other 24 B in addr6
+          const uint8_t* a = &addr6_[(c * RTN_CHUNK_FRAMES + k6) * 24u];
           x.src.v6 = x.dst.v6 = true;
-          std::memcpy(x.src.ip, a, 16);
-          std::memcpy(x.dst.ip, a + 16, 16);
-          if (tcp) {  // an IPv6 TCP record holds seq / ack in place of the addresses
-            x.seq_no = r.w0;
-            x.ack_no = r.w1;
-          }
+          std::memcpy(x.src.ip, &r.w0, 4);
+          std::memcpy(x.src.ip + 4, &r.w1, 4);
+          std::memcpy(x.src.ip + 8, a, 8);
+          std::memcpy(x.dst.ip, a + 8, 16);
           ++k6;
         } else {
           for (int j = 0; j < 4; ++j) {
             x.src.ip[j] = (uint8_t)(r.w0 >> (24 - 8 * j));
             x.dst.ip[j] = (uint8_t)(r.w1 >> (24 - 8 * j));
           }
-          if (tcp) {  // IPv4 TCP: the tcp4 side stream, ranked among the chunk's IPv4 TCP records
-            const uint64_t t = tcp4_[RTN_REC_INDEX(n_, c, k4)];
-            x.seq_no = RTN_TCP4_SEQ(t);
-            x.ack_no = RTN_TCP4_ACK(t);
-            ++k4;
-          }
+        }
+        if (tcp) {  // the seqack side stream, ranked among the chunk's TCP records
+          const uint64_t t = seqack_[RTN_REC_INDEX(n_, c, kt)];
+          x.seq_no = RTN_SEQACK_SEQ(t);
+          x.ack_no = RTN_SEQACK_ACK(t);
+          ++kt;
         }
         f(i, x);
         ++k;
@@ -184,7 +182,7 @@ class Burst {
   uint32_t words_ = 0;
   std::vector<uint64_t> pc_, fwd_, dlv_, dlv_recs_;
   std::vector<rtn_l4ctx_t> l4_;
-  std::vector<uint64_t> tcp4_;
+  std::vector<uint64_t> seqack_;
   std::vector<uint8_t> addr6_;
   const std::vector<CallbackSite>* sites_ = nullptr;
   Stats stats_;
@@ -240,7 +238,7 @@ class Subscription {
     o.fwd_bitmap = d_fwd_;
     o.l4 = reinterpret_cast<rtn_l4ctx_t*>(d_l4_);
     o.addr6 = d_addr6_;
-    o.tcp4 = d_tcp4_;
+    o.seqack = d_seqack_;
     o.dlv_bitmap = info_.deliver_words ? d_dlv_ : nullptr;
     o.dlv_records = info_.deliver_words ? d_dlv_recs_ : nullptr;
     o.counters = d_counters_;
@@ -255,13 +253,13 @@ class Subscription {
     b.fwd_.resize(bm / 8);
     b.l4_.resize(rtn_out_l4_bytes(in.n) / sizeof(rtn_l4ctx_t));
     b.addr6_.resize(rtn_out_addr6_bytes(in.n));
-    b.tcp4_.resize(rtn_out_tcp4_bytes(in.n) / 8);
+    b.seqack_.resize(rtn_out_seqack_bytes(in.n) / 8);
     uint32_t cnt[RTN_COUNTERS_BYTES / 4];
     d2h(b.pc_.data(), d_pc_, bm, stream);
     d2h(b.fwd_.data(), d_fwd_, bm, stream);
     d2h(b.l4_.data(), d_l4_, b.l4_.size() * sizeof(rtn_l4ctx_t), stream);
     d2h(b.addr6_.data(), d_addr6_, b.addr6_.size(), stream);
-    d2h(b.tcp4_.data(), d_tcp4_, b.tcp4_.size() * 8, stream);
+    d2h(b.seqack_.data(), d_seqack_, b.seqack_.size() * 8, stream);
     d2h(cnt, d_counters_, sizeof(cnt), stream);
     if (info_.deliver_words) {
       b.dlv_.resize(bm / 8);
@@ -298,10 +296,10 @@ class Subscription {
   }
   void release() {
     for (void* p : {static_cast<void*>(d_pc_), static_cast<void*>(d_fwd_), d_l4_, static_cast<void*>(d_addr6_),
-                    static_cast<void*>(d_tcp4_), static_cast<void*>(d_dlv_), static_cast<void*>(d_dlv_recs_),
+                    static_cast<void*>(d_seqack_), static_cast<void*>(d_dlv_), static_cast<void*>(d_dlv_recs_),
                     static_cast<void*>(d_counters_)})
       if (p) (void)hipFree(p);
-    d_pc_ = d_fwd_ = d_dlv_ = d_dlv_recs_ = d_tcp4_ = nullptr;
+    d_pc_ = d_fwd_ = d_dlv_ = d_dlv_recs_ = d_seqack_ = nullptr;
     d_l4_ = nullptr;
     d_addr6_ = nullptr;
     d_counters_ = nullptr;
@@ -314,7 +312,7 @@ class Subscription {
     d_fwd_ = static_cast<uint64_t*>(dalloc(rtn_out_bitmap_bytes(n)));
     d_l4_ = dalloc(rtn_out_l4_bytes(n));
     d_addr6_ = static_cast<uint8_t*>(dalloc(rtn_out_addr6_bytes(n)));
-    d_tcp4_ = static_cast<uint64_t*>(dalloc(rtn_out_tcp4_bytes(n)));
+    d_seqack_ = static_cast<uint64_t*>(dalloc(rtn_out_seqack_bytes(n)));
     if (info_.deliver_words) {
       d_dlv_ = static_cast<uint64_t*>(dalloc(rtn_out_bitmap_bytes(n)));
       d_dlv_recs_ = static_cast<uint64_t*>(dalloc(rtn_out_dlv_bytes(n, info_.deliver_words)));
@@ -330,7 +328,7 @@ class Subscription {
   std::vector<CallbackSite> sites_;
   Stats stats_;
   uint32_t cap_ = 0;
-  uint64_t *d_pc_ = nullptr, *d_fwd_ = nullptr, *d_dlv_ = nullptr, *d_dlv_recs_ = nullptr, *d_tcp4_ = nullptr;
+  uint64_t *d_pc_ = nullptr, *d_fwd_ = nullptr, *d_dlv_ = nullptr, *d_dlv_recs_ = nullptr, *d_seqack_ = nullptr;
   void* d_l4_ = nullptr;
   uint8_t* d_addr6_ = nullptr;
   uint32_t* d_counters_ = nullptr;

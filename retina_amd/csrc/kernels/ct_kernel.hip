@@ -48,7 +48,7 @@ typedef unsigned long long rtn_u64;
 struct rtn_ct_args {
   const rtn_u64* fwd_bm;
   const rtn_u32* recs;        // rtn_l4ctx_t, 4 words each (w0, w1, ports, meta)
-  const rtn_u32* addr6;       // 8 words per IPv6 record
+  const rtn_u32* addr6;       // 6 words per IPv6 record (source bytes 8..15, destination)
   const rtn_u64* conn;        // rtn_conn_t
   rtn_u64* out;               // rtn_ct_entry_t (slot | status << 32), indexed like recs
   rtn_u32* table;             // cap * 16 words
@@ -97,10 +97,11 @@ __device__ __forceinline__ void rtn_ct_make_key(const rtn_ct_args& a, const rtn_
   k.tcp = !((meta >> 6) & 1u);
   const bool gt = (k.info >> 27) & 1u;  // src is the max endpoint
   rtn_u32 s[4], d[4];
-  if (k.v6) {
-    const uint4 x = reinterpret_cast<const uint4*>(a6)[0], y = reinterpret_cast<const uint4*>(a6)[1];
-    s[0] = __builtin_bswap32(x.x); s[1] = __builtin_bswap32(x.y); s[2] = __builtin_bswap32(x.z); s[3] = __builtin_bswap32(x.w);
-    d[0] = __builtin_bswap32(y.x); d[1] = __builtin_bswap32(y.y); d[2] = __builtin_bswap32(y.z); d[3] = __builtin_bswap32(y.w);
+  if (k.v6) {  // source bytes 0..7 in the record, 8..15 and the destination in addr6 (24 B, 8-B aligned)
+    const uint2 x = reinterpret_cast<const uint2*>(a6)[0], y = reinterpret_cast<const uint2*>(a6)[1],
+                z = reinterpret_cast<const uint2*>(a6)[2];
+    s[0] = __builtin_bswap32(rec[0]); s[1] = __builtin_bswap32(rec[1]); s[2] = __builtin_bswap32(x.x); s[3] = __builtin_bswap32(x.y);
+    d[0] = __builtin_bswap32(y.x); d[1] = __builtin_bswap32(y.y); d[2] = __builtin_bswap32(z.x); d[3] = __builtin_bswap32(z.y);
   } else {
     s[0] = rec[0];
     d[0] = rec[1];
@@ -293,7 +294,7 @@ __device__ __forceinline__ void rtn_ct_item_key(const rtn_ct_args& a, const rtn_
     rec[2 * j + 1] = (rtn_u32)(x >> 32);
   }
   const bool v6 = (it.cv >> 61) & 1ull;
-  rtn_ct_make_key(a, rec, it.cv, v6 ? a.addr6 + ((rtn_u64)ch.c * RTN_CT_CHUNK + it.v6r) * 8u : nullptr, k);
+  rtn_ct_make_key(a, rec, it.cv, v6 ? a.addr6 + ((rtn_u64)ch.c * RTN_CT_CHUNK + it.v6r) * 6u : nullptr, k);
 }
 
 extern "C" __global__ void __launch_bounds__(64u * RTN_CT_CPB) rtn_ct_insert(rtn_ct_args a) {

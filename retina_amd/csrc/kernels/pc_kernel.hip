@@ -50,14 +50,15 @@ typedef unsigned int rtn_v4u __attribute__((ext_vector_type(4)));
 #define RTN_LD_STREAM(p) __builtin_nontemporal_load(p)
 
 struct rtn_l4rec {       // 16 B, the compacted L4Context of a forwarded packet (rtn_l4ctx_t)
-  rtn_u32 w0;            // IPv4: u32::from(src Ipv4Addr); IPv6 TCP: seq_no; IPv6 UDP: 0
-  rtn_u32 w1;            // IPv4: dst; IPv6 TCP: ack_no; IPv6 UDP: 0
+  rtn_u32 w0;            // IPv4: u32::from(src Ipv4Addr); IPv6: source address bytes 0..3 (raw)
+  rtn_u32 w1;            // IPv4: dst; IPv6: source address bytes 4..7 (raw)
   rtn_u32 ports;         // src_port | dst_port << 16
   rtn_u32 meta;          // offset >> 2 | udp << 6 | ipv6 << 7 | tcp flags << 8 | length << 16
 };
-// IPv4 TCP records keep seq_no | ack_no << 32 in the tcp4 side stream (rtn_pc_out_t.tcp4), ranked
-// among the chunk's IPv4 TCP records: no record carries a field that is always zero for its kind
-// (UDP has no seq/ack, IPv6 keeps its addresses in addr6; pdu.rs:66-84).
+// TCP records keep seq_no | ack_no << 32 in the seqack side stream (rtn_pc_out_t.seqack), ranked
+// among the chunk's TCP records; IPv6 records the rest of their addresses (source bytes 8..15,
+// destination) in addr6, 24 B each: no record carries a field that is always zero for its kind
+// (UDP has no seq/ack; pdu.rs:66-84).
 
 struct rtn_args {
   const unsigned char* slab;
@@ -65,13 +66,14 @@ struct rtn_args {
   const unsigned short* dlen;
   rtn_u32 n;
   rtn_u32 flags;              // bit0: addr6, bit1: counters, bit2: conn, bit3: caller asserts data_len <= 64,
-                              // bit4: compact ext rows (RTN_BATCH_EXT_COMPACT), bit5: tcp4
+                              // bit4: compact ext rows (RTN_BATCH_EXT_COMPACT), bit5: seqack
   rtn_u64* pc_bm;             // [ceil(n/64)]  PacketContinue bit
   rtn_u64* fwd_bm;            // [ceil(n/64)]  PacketContinue && L4Context::new Ok
   rtn_l4rec* recs;            // [ceil(n/256)*256] at RTN_REC_INDEX
-  unsigned char* addr6;       // [ceil(n/256)*256][32] (rtn_out_addr6_bytes) (src, dst) raw bytes, IPv6
-                              // records only; rtn_flush6 pads a chunk's last store to whole lines,
-                              // up to 3 entries past its last record (inside the chunk's 256)
+  unsigned char* addr6;       // [ceil(n/256)*256][24] (rtn_out_addr6_bytes) source bytes 8..15 and
+                              // destination (raw) of the IPv6 records; rtn_flush6 pads a chunk's
+                              // last store to whole 64-B requests, up to 2 entries past its last
+                              // record (inside the chunk's 256)
   rtn_u64* dlv_bm;            // [ceil(n/64)]  any packet-level delivery
   rtn_u64* dlv_recs;          // [ceil(n/256)*256][RTN_DELIVER_WORDS] statement masks, ranked by dlv_bm per chunk
   rtn_u32* counters;          // [0] pc, [1] fwd, [2] dlv, [3] status, [4..5] bytes, [6..7] ignored bytes,
@@ -82,8 +84,8 @@ struct rtn_args {
   const rtn_u32* ext_chunk;   // flags bit4 (compact ext): row of each chunk's first needing frame
   rtn_u32 ext_rows;           // ... and the rows ext holds
   rtn_u32 cpw;                // compact split kernel: consecutive chunks per wave (1 or 2)
-  rtn_u64* tcp4;              // optional [ceil(n/256)*256] seq | ack << 32 of the IPv4 TCP records, at
-                              // RTN_REC_INDEX of their rank among the chunk's IPv4 TCP records (bit5)
+  rtn_u64* seqack;            // optional [ceil(n/256)*256] seq | ack << 32 of the TCP records, at
+                              // RTN_REC_INDEX of their rank among the chunk's TCP records (bit5)
 };
 
 struct rtn_view {
@@ -371,7 +373,7 @@ struct rtn_chunk {
   rtn_u32 ndlv;             // delivery records produced in this chunk
   rtn_u32 nv6, nv6flushed;  // IPv6 address records (addr6) produced / stored in this chunk
   rtn_u32 next;             // compact ext: needing frames of this chunk so far
-  rtn_u32 ntcp, ntflushed;  // IPv4 TCP records (tcp4 side stream) produced / stored in this chunk
+  rtn_u32 ntcp, ntflushed;  // TCP records (seqack side stream) produced / stored in this chunk
   rtn_u64 my_pc, my_fwd, my_dlv;  // lane k holds group k's bitmap words until the chunk ends
 };
 
@@ -419,25 +421,25 @@ __device__ __forceinline__ void rtn_flush(const rtn_args& a, const rtn_u64* ring
   if (lane < nl) RTN_ST(dst + (lane / RTN_RB) * nch * RTN_RB + lane % RTN_RB, src[lane]);
 }
 
-// seq/ack entries of IPv4 TCP records [ntflushed, ntflushed + nent): 8 B each, two per lane,
-// whole 64-B requests, 64-entry blocks at RTN_REC_INDEX of the chunk's IPv4-TCP rank.
+// seq/ack entries of TCP records [ntflushed, ntflushed + nent): 8 B each, two per lane, whole
+// 64-B requests, 64-entry blocks at RTN_REC_INDEX of the chunk's TCP rank.
 __device__ __forceinline__ void rtn_flush_t4(const rtn_args& a, const rtn_u64* ring4, const rtn_chunk& ch,
                                              rtn_u32 lane, rtn_u32 nent) {
   const rtn_u64 nch = rtn_nchunks(a.n);
   const rtn_u32 nl = ((nent + 1u) / 2u + 3u) & ~3u;
   const rtn_v4u* src = reinterpret_cast<const rtn_v4u*>(ring4 + (ch.ntflushed & (RTN_RING - 1u)));
-  rtn_v4u* dst = reinterpret_cast<rtn_v4u*>(a.tcp4 + rtn_rec_slot(nch, ch.rec_base / (64u * RTN_CHUNK_GROUPS), ch.ntflushed));
+  rtn_v4u* dst = reinterpret_cast<rtn_v4u*>(a.seqack + rtn_rec_slot(nch, ch.rec_base / (64u * RTN_CHUNK_GROUPS), ch.ntflushed));
   if (lane < nl) RTN_ST(dst + (lane / (RTN_RB / 2u)) * nch * (RTN_RB / 2u) + lane % (RTN_RB / 2u), src[lane]);
 }
 
-// IPv6 address records (32 B: src, dst) are dense per chunk over the chunk's forwarded IPv6
-// frames. Where IPv6 is common (the split / wide-slot kernels) they leave through their own
-// per-wave LDS ring (96 entries, 3 KB) in whole 1-KB blocks: scattered 32-B stores with holes
-// between them cost about 4x their bytes in HBM time. A group adds up to 64 entries, so the ring
-// holds them on top of the < 32 a group starts with. (A 128-entry ring holds the block to 3 per
-// CU by LDS: cfg4 0.2028 -> 0.1942 ms with 64, in-process A/B; 96 keeps 4 now that the packet
-// stage without the connection stage has no conn ring. A 64-entry ring needs a second store pass
-// in IPv6-dense groups: cfg3 +2 %.)
+// IPv6 address records (24 B: source bytes 8..15, destination; the record holds source bytes
+// 0..7) are dense per chunk over the chunk's forwarded IPv6 frames. Where IPv6 is common (the
+// split / wide-slot kernels) they leave through their own per-wave LDS ring (96 entries, 2.25 KB)
+// in whole 768-B blocks: scattered stores with holes between them cost about 4x their bytes in HBM
+// time. A group adds up to 64 entries, so the ring holds them on top of the < 32 a group starts
+// with. (A 128-entry ring of the 32-B entries held the block to 3 per CU by LDS: cfg4 0.2028 ->
+// 0.1942 ms with 64, in-process A/B; a 64-entry ring needs a second store pass in IPv6-dense
+// groups: cfg3 +2 %.)
 #define RTN_RING6 96u
 #define RTN_FLUSH6 32u
 
@@ -445,18 +447,23 @@ __device__ __forceinline__ void rtn_flush_t4(const rtn_args& a, const rtn_u64* r
 // below 64): one subtract and a min instead of the modulo's quarter-rate multiplies.
 __device__ __forceinline__ rtn_u32 rtn_ring6_at(rtn_u32 x) { return min(x, x - RTN_RING6); }
 
-// Stores ring entries [nv6flushed, nv6flushed + nent) (nent <= RTN_RING6), rounded up to whole
-// 64-B write requests (2 entries): a partial request costs a read-modify-write. Only a chunk's last store is
+// Stores ring entries [nv6flushed, nv6flushed + nent) (nent <= 64; nv6flushed is a multiple
+// of RTN_FLUSH6, so the run starts on a 16-B unit of the ring and of addr6), rounded up to whole
+// 64-B write requests: a partial request costs a read-modify-write. Only a chunk's last store is
 // partial, and its padding (stale ring bytes) lands in the chunk's unused addr6 space, as for the
-// record blocks.
+// record blocks. The ring is 96 x 24 B = 144 16-B units, so a unit never straddles its wrap.
 __device__ __forceinline__ void rtn_flush6(const rtn_args& a, const rtn_v4u* ring6, const rtn_chunk& ch, rtn_u32 lane,
                                            rtn_u32 nent) {
-  const rtn_u32 nv4 = ((nent + 1u) & ~1u) * 2u;  // 16-B halves
-  rtn_v4u* dst = reinterpret_cast<rtn_v4u*>(a.addr6 + (ch.rec_base + ch.nv6flushed) * 32u);
+  const rtn_u32 nu = ((nent * 24u + 63u) & ~63u) / 16u;  // 16-B units, whole 64-B requests
+  const rtn_u32 u0 = (ch.nv6flushed % RTN_RING6) * 24u / 16u;
+  rtn_v4u* dst = reinterpret_cast<rtn_v4u*>(a.addr6 + (ch.rec_base + ch.nv6flushed) * 24u);
 #pragma unroll
   for (rtn_u32 j = 0; j < 2u; ++j) {
     const rtn_u32 k = lane + 64u * j;
-    if (k < nv4) RTN_ST(dst + k, ring6[rtn_ring6_at(ch.nv6flushed % RTN_RING6 + k / 2u) * 2u + (k & 1u)]);
+    if (k < nu) {
+      const rtn_u32 u = u0 + k;
+      RTN_ST(dst + k, ring6[min(u, u - RTN_RING6 * 24u / 16u)]);
+    }
   }
 }
 
@@ -494,8 +501,8 @@ __device__ __forceinline__ void rtn_group(const rtn_args& a, rtn_u32 g, rtn_u32 
   acc.udpb += (fwd && !v.tcp) ? dl : 0u;
   ch.my_pc = lane == k ? pcm : ch.my_pc;
   ch.my_fwd = lane == k ? fwdm : ch.my_fwd;
-  // IPv4 TCP records: their seq/ack go to the tcp4 side stream (when requested)
-  const bool t4 = fwd && v.v4 && v.tcp && (a.flags & 32u);
+  // TCP records: their seq/ack go to the seqack side stream (when requested)
+  const bool t4 = fwd && v.tcp && (a.flags & 32u);
   const rtn_u64 t4m = __ballot(t4);
   if (fwd) {
     const rtn_u32 r = ch.nrec + (rtn_u32)__popcll(fwdm & lane_lt);
@@ -511,7 +518,7 @@ __device__ __forceinline__ void rtn_group(const rtn_args& a, rtn_u32 g, rtn_u32 
     const rtn_u32 ports = rtn_l4_be16(v, 0) | (rtn_l4_be16(v, 2) << 16);
     const rtn_u32 seq = tcp ? rtn_l4_be32(v, 4) : 0u, ack = tcp ? rtn_l4_be32(v, 8) : 0u;
     rtn_u64* rp = ring + (r & (RTN_RING - 1u)) * 2u;
-    rp[0] = v.v4 ? ((rtn_u64)src4 | ((rtn_u64)dst4 << 32)) : ((rtn_u64)seq | ((rtn_u64)ack << 32));
+    rp[0] = v.v4 ? ((rtn_u64)src4 | ((rtn_u64)dst4 << 32)) : ((rtn_u64)v.l3w[2] | ((rtn_u64)v.l3w[3] << 32));
     rp[1] = (rtn_u64)ports | ((rtn_u64)meta << 32);
     if (t4) ring4[(ch.ntcp + (rtn_u32)__popcll(t4m & lane_lt)) & (RTN_RING - 1u)] = (rtn_u64)seq | ((rtn_u64)ack << 32);
     if (CONN) {
@@ -583,15 +590,16 @@ __device__ __forceinline__ void rtn_group(const rtn_args& a, rtn_u32 g, rtn_u32 
   const rtn_u64 m6 = __ballot(six);
   const rtn_u32 rank6 = (rtn_u32)__popcll(m6 & lane_lt), cnt6 = (rtn_u32)__popcll(m6);
   const rtn_u32 r6 = ch.nv6 + rank6;
-  const rtn_v4u s0 = rtn_v4u{v.l3w[2], v.l3w[3], v.l3w[4], v.l3w[5]};
-  const rtn_v4u s1 = rtn_v4u{v.l3w[6], v.l3w[7], v.l3w[8], v.l3w[9]};
+  const rtn_u64 s0 = (rtn_u64)v.l3w[4] | ((rtn_u64)v.l3w[5] << 32), s1 = (rtn_u64)v.l3w[6] | ((rtn_u64)v.l3w[7] << 32),
+                s2 = (rtn_u64)v.l3w[8] | ((rtn_u64)v.l3w[9] << 32);
   if (STAGE6) {
     // Fewer than RTN_FLUSH6 entries are pending when a group starts (every whole block is stored
     // below), so the group's at most 64 entries always find free slots in the 96-entry ring.
     if (six) {
-      const rtn_u32 at = rtn_ring6_at(ch.nv6 % RTN_RING6 + rank6);
-      ring6[at * 2u] = s0;
-      ring6[at * 2u + 1u] = s1;
+      rtn_u64* e = reinterpret_cast<rtn_u64*>(ring6) + rtn_ring6_at(ch.nv6 % RTN_RING6 + rank6) * 3u;
+      e[0] = s0;
+      e[1] = s1;
+      e[2] = s2;
     }
     ch.nv6 += cnt6;
     if (ch.nv6 - ch.nv6flushed >= RTN_FLUSH6) {  // every whole block pending (at most 64 entries)
@@ -603,9 +611,10 @@ __device__ __forceinline__ void rtn_group(const rtn_args& a, rtn_u32 g, rtn_u32 
     }
   } else {
     if (six) {
-      rtn_v4u* ap = reinterpret_cast<rtn_v4u*>(a.addr6 + (ch.rec_base + r6) * 32u);
+      rtn_u64* ap = reinterpret_cast<rtn_u64*>(a.addr6 + (ch.rec_base + r6) * 24u);
       ap[0] = s0;
       ap[1] = s1;
+      ap[2] = s2;
     }
     ch.nv6 += cnt6;
   }
@@ -664,12 +673,12 @@ __device__ __forceinline__ void rtn_run(const rtn_args& a) {
   rtn_acc acc = {0u, 0u, 0u, 0u, 0u, 0ull, 0ull, 0ull, 0ull};
   __shared__ __attribute__((aligned(16))) rtn_u64 rtn_ring[4][RTN_RING * 2u];
   rtn_u64* ring = rtn_ring[threadIdx.x >> 6];
-  __shared__ __attribute__((aligned(16))) rtn_u64 rtn_ring4[4][RTN_RING];  // IPv4 TCP seq/ack
+  __shared__ __attribute__((aligned(16))) rtn_u64 rtn_ring4[4][RTN_RING];  // TCP seq/ack
   rtn_u64* ring4 = rtn_ring4[threadIdx.x >> 6];
   __shared__ __attribute__((aligned(16))) rtn_u64 rtn_cring[4][CONN ? RTN_RING : 2u];  // connection-stage entries
   rtn_u64* cring = rtn_cring[threadIdx.x >> 6];
   constexpr bool stage6 = MODE != RTN_S64;  // 64-byte slots rarely forward IPv6 (only short UDP)
-  __shared__ __attribute__((aligned(16))) rtn_v4u rtn_ring6[4][stage6 ? RTN_RING6 * 2u : 1u];
+  __shared__ __attribute__((aligned(16))) rtn_v4u rtn_ring6[4][stage6 ? RTN_RING6 * 24u / 16u : 1u];
   rtn_v4u* ring6 = rtn_ring6[threadIdx.x >> 6];
   __shared__ __attribute__((aligned(16))) rtn_u32 rtn_tile[4][slots64 ? 64 * RTN_XPITCH : 1];
   rtn_u32* tile = rtn_tile[threadIdx.x >> 6];
@@ -939,7 +948,7 @@ extern "C" __global__ void __launch_bounds__(RTN_PD_THREADS) rtn_pd_kernel(rtn_p
       c.v4 = !v6;
       c.udp = (rec[u][3] >> 6) & 1u;
       c.tcp = !c.udp;
-      c.src4 = v6 ? 0u : rec[u][0];  // (an IPv6 TCP record holds seq / ack there)
+      c.src4 = v6 ? 0u : rec[u][0];  // (an IPv6 record holds its source's first 8 bytes there)
       c.dst4 = v6 ? 0u : rec[u][1];
       c.sport = rec[u][2] & 0xffffu;
       c.dport = rec[u][2] >> 16;
@@ -948,13 +957,14 @@ extern "C" __global__ void __launch_bounds__(RTN_PD_THREADS) rtn_pd_kernel(rtn_p
         c.s6[j] = 0u;
         c.d6[j] = 0u;
       }
-      if (v6) {
-        const rtn_u32* ap = reinterpret_cast<const rtn_u32*>(a.addr6 + r6 * 32u);
+      if (v6) {  // source bytes 0..7 in the record, 8..15 and the destination in addr6 (24 B)
+        const rtn_u32* ap = reinterpret_cast<const rtn_u32*>(a.addr6 + r6 * 24u);
+        c.s6[0] = __builtin_bswap32(rec[u][0]);
+        c.s6[1] = __builtin_bswap32(rec[u][1]);
+        c.s6[2] = __builtin_bswap32(ap[0]);
+        c.s6[3] = __builtin_bswap32(ap[1]);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          c.s6[j] = __builtin_bswap32(ap[j]);
-          c.d6[j] = __builtin_bswap32(ap[4 + j]);
-        }
+        for (int j = 0; j < 4; ++j) c.d6[j] = __builtin_bswap32(ap[2 + j]);
       }
       // Payload::from_mbuf (datatypes/src/packet.rs:18-29): get_data_slice(offset, length)
       const rtn_u32 dlen = a.dlen[(ch * RTN_CHUNK_GROUPS + q) * 64u + lane];

@@ -263,7 +263,7 @@ struct KArgs {
   const uint32_t* ext_chunk;
   uint32_t ext_rows;
   uint32_t cpw;
-  uint64_t* tcp4;
+  uint64_t* seqack;
 };
 
 // Groups per wave of a kernel (RTN_PD_GPW / RTN_CT_GPW): the default, unless an RTN_KERNEL_DEFINES
@@ -658,8 +658,8 @@ int32_t rtn_pc_run(rtn_pc_t* pc, const rtn_batch_t* in, rtn_pc_out_t* out, void*
   if (in->stride == 64 && !in->ext && !(in->flags & RTN_BATCH_DL_LE64) && !out->counters)
     return fail(RTN_EINVAL, "64-byte slots without ext need RTN_BATCH_DL_LE64 (every data_len <= 64) or counters");
   // record arrays leave in 16-B-per-lane stores
-  for (const void* o : {(const void*)out->l4, (const void*)out->addr6, (const void*)out->conn, (const void*)out->tcp4})
-    if ((reinterpret_cast<uintptr_t>(o) & 15u) != 0) return fail(RTN_EINVAL, "l4/addr6/conn/tcp4 must be 16-byte aligned");
+  for (const void* o : {(const void*)out->l4, (const void*)out->addr6, (const void*)out->conn, (const void*)out->seqack})
+    if ((reinterpret_cast<uintptr_t>(o) & 15u) != 0) return fail(RTN_EINVAL, "l4/addr6/conn/seqack must be 16-byte aligned");
   const uint32_t dw = pc->program->prog.deliver_words();
   if (dw > 0 && (!out->dlv_bitmap || !out->dlv_records))
     return fail(RTN_EINVAL, "program has packet-level callbacks: dlv_bitmap/dlv_records required");
@@ -678,8 +678,8 @@ int32_t rtn_pc_run(rtn_pc_t* pc, const rtn_batch_t* in, rtn_pc_out_t* out, void*
   a.n = in->n;
   a.flags = (out->addr6 ? 1u : 0u) | (out->counters ? 2u : 0u) | (out->conn ? 4u : 0u) |
             ((in->flags & RTN_BATCH_DL_LE64) ? 8u : 0u) | ((in->flags & RTN_BATCH_EXT_COMPACT) ? 16u : 0u) |
-            (out->tcp4 ? 32u : 0u);
-  a.tcp4 = out->tcp4;
+            (out->seqack ? 32u : 0u);
+  a.seqack = out->seqack;
   a.ext_chunk = in->ext_chunk;
   a.ext_rows = in->ext_rows;
   a.cpw = (in->ext && (in->flags & RTN_BATCH_EXT_COMPACT)) ? (out->conn ? pc->splitc_cpw_conn : pc->splitc_cpw) : 1u;
@@ -801,8 +801,8 @@ size_t rtn_out_bitmap_bytes(uint32_t n) { return (((size_t)n + 63u) / 64u) * 8u;
 static size_t chunked(uint32_t n) { return (((size_t)n + RTN_CHUNK_FRAMES - 1u) / RTN_CHUNK_FRAMES) * RTN_CHUNK_FRAMES; }
 static_assert(sizeof(rtn_l4ctx_t) == 16, "rtn_l4ctx_t is 16 bytes");
 size_t rtn_out_l4_bytes(uint32_t n) { return chunked(n) * sizeof(rtn_l4ctx_t); }
-size_t rtn_out_tcp4_bytes(uint32_t n) { return chunked(n) * 8u; }
-size_t rtn_out_addr6_bytes(uint32_t n) { return chunked(n) * 32u; }
+size_t rtn_out_seqack_bytes(uint32_t n) { return chunked(n) * 8u; }
+size_t rtn_out_addr6_bytes(uint32_t n) { return chunked(n) * 24u; }
 size_t rtn_out_dlv_bytes(uint32_t n, uint32_t deliver_words) {
   return chunked(n) * (size_t)deliver_words * 8u;
 }

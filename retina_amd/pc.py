@@ -46,7 +46,7 @@ MAX_FRAMES = 1 << 31       # RTN_MAX_FRAMES
 class _Out(C.Structure):
     _fields_ = [("pc_bitmap", C.c_void_p), ("fwd_bitmap", C.c_void_p), ("l4", C.c_void_p),
                 ("addr6", C.c_void_p), ("dlv_bitmap", C.c_void_p), ("dlv_records", C.c_void_p),
-                ("counters", C.c_void_p), ("conn", C.c_void_p), ("conn_dlv", C.c_void_p), ("tcp4", C.c_void_p)]
+                ("counters", C.c_void_p), ("conn", C.c_void_p), ("conn_dlv", C.c_void_p), ("seqack", C.c_void_p)]
 
 
 class _PcapStats(C.Structure):
@@ -110,7 +110,7 @@ EXPORTS = {
     "rtn_out_dlv_bytes": (C.c_size_t, [C.c_uint32, C.c_uint32]),
     "rtn_out_conn_bytes": (C.c_size_t, [C.c_uint32]),
     "rtn_out_conn_dlv_bytes": (C.c_size_t, [C.c_uint32, C.c_uint32]),
-    "rtn_out_tcp4_bytes": (C.c_size_t, [C.c_uint32]),
+    "rtn_out_seqack_bytes": (C.c_size_t, [C.c_uint32]),
     # include/retina_ct.h
     "rtn_ct_create": (C.c_int32, [C.c_int, C.c_uint32, C.c_uint32, C.POINTER(C.c_void_p)]),
     "rtn_ct_destroy": (C.c_int32, [C.c_void_p]),
@@ -182,8 +182,9 @@ def _text(fn, h) -> str:
     return buf.value.decode()
 
 
-# rtn_l4ctx_t (include/retina_pc.h), 16 bytes: w0/w1 = IPv4 addresses, or an IPv6 TCP record's
-# seq/ack; IPv4 TCP seq/ack in the tcp4 side stream
+# rtn_l4ctx_t (include/retina_pc.h), 16 bytes: w0/w1 = IPv4 addresses, or an IPv6 record's source
+# address bytes 0..7 (the rest of its addresses in addr6, 24 B); TCP seq/ack in the seqack side
+# stream
 L4_DTYPE = np.dtype([("w0", "<u4"), ("w1", "<u4"), ("ports", "<u4"), ("meta", "<u4")])
 # what PCOutputs.decode() returns per forwarded frame: the record's fields unpacked, plus the
 # frame index its position implies
@@ -192,24 +193,21 @@ L4_DECODED = np.dtype([("pkt_idx", "<u8"), ("src_ip4", "<u4"), ("dst_ip4", "<u4"
                        ("length", "<u4"), ("proto", "<u4"), ("flags", "<u4"), ("ver", "<u4")])
 
 
-def decode_l4(raw: np.ndarray, frames: np.ndarray, tcp4: np.ndarray | None = None, n: int | None = None) -> np.ndarray:
+def decode_l4(raw: np.ndarray, frames: np.ndarray, seqack: np.ndarray | None = None, n: int | None = None) -> np.ndarray:
     """Unpack rtn_l4ctx_t records (the RTN_L4_* accessors of retina_pc.h) of the forwarded frames
-    `frames` (ascending); `tcp4` is the run's tcp4 side stream (uint64) for the IPv4 TCP records'
-    seq/ack (left 0 when None), n the batch size."""
+    `frames` (ascending); `seqack` is the run's seqack side stream (uint64) for the TCP records'
+    seq/ack (left 0 when None), n the batch size. IPv6 addresses: PCOutputs.decode()."""
     out = np.zeros(len(raw), L4_DECODED)
     out["pkt_idx"] = frames
     m = raw["meta"]
     v6, udp = (m & 0x80) != 0, (m & 0x40) != 0
     out["src_ip4"] = np.where(v6, 0, raw["w0"])
     out["dst_ip4"] = np.where(v6, 0, raw["w1"])
-    t6 = v6 & ~udp  # IPv6 TCP: seq / ack in the record
-    out["seq_no"][t6] = raw["w0"][t6]
-    out["ack_no"][t6] = raw["w1"][t6]
-    t4 = ~v6 & ~udp
-    if tcp4 is not None and t4.any():
-        t = tcp4[_rec_index(np.asarray(frames, np.int64)[t4], n)]
-        out["seq_no"][t4] = (t & 0xFFFFFFFF).astype(np.uint32)
-        out["ack_no"][t4] = (t >> 32).astype(np.uint32)
+    tcp = ~udp
+    if seqack is not None and tcp.any():
+        t = seqack[_rec_index(np.asarray(frames, np.int64)[tcp], n)]
+        out["seq_no"][tcp] = (t & 0xFFFFFFFF).astype(np.uint32)
+        out["ack_no"][tcp] = (t >> 32).astype(np.uint32)
     out["sport"] = raw["ports"] & 0xFFFF
     out["dport"] = raw["ports"] >> 16
     out["offset"] = ((m & 0x3F) << 2) | 2
@@ -356,7 +354,7 @@ class PCOutputs:
     conn: object = None
     conn_dlv: object = None
     conn_words: int = 0
-    tcp4: object = None
+    seqack: object = None
 
     def counters_host(self) -> np.ndarray:
         """[pc, fwd, dlv, status] (uint32)."""
@@ -386,15 +384,18 @@ class PCOutputs:
         fwd = np.unpackbits(fwd_bm.view(np.uint8), bitorder="little")[:n].astype(bool)
         recs_all = self.l4.cpu().numpy().view(L4_DTYPE)
         idx = _fwd_index(fwd_bm, n)
-        t4 = self.tcp4.cpu().numpy().view(np.uint64) if self.tcp4 is not None else None
+        t4 = self.seqack.cpu().numpy().view(np.uint64) if self.seqack is not None else None
         recs = decode_l4(recs_all[idx], np.nonzero(fwd)[0], t4, n)
         out = {"pc": pc, "fwd": fwd, "l4": recs}
         if self.addr6 is not None:
-            # dense per chunk over the chunk's forwarded IPv6 frames; one row per record here
-            a6 = self.addr6.cpu().numpy().view(np.uint8).reshape(-1, 32)
+            # src | dst (32 B) per record: source bytes 0..7 from the record, the other 24 B from
+            # addr6, dense per chunk over the chunk's forwarded IPv6 frames
+            a6 = self.addr6.cpu().numpy().view(np.uint8).reshape(-1, 24)
             v6 = recs["ver"] == 6
             rows = np.zeros((len(recs), 32), np.uint8)
-            rows[v6] = a6[_rank_index(recs["pkt_idx"][v6].astype(np.int64))]
+            r6 = recs_all[idx][v6]
+            rows[v6, :8] = np.stack([r6["w0"], r6["w1"]], axis=1).astype("<u4").view(np.uint8).reshape(-1, 8)
+            rows[v6, 8:] = a6[_rank_index(recs["pkt_idx"][v6].astype(np.int64))]
             out["addr6"] = rows
         if self.conn is not None:
             c = self.conn.cpu().numpy().view(np.uint32).reshape(-1, 2)[idx]
@@ -505,7 +506,7 @@ class PacketContinue:
         return idx[:k], cb
 
     def alloc_outputs(self, n: int, addr6: bool = True, counters: bool = True, conn: bool = False,
-                      tcp4: bool = True) -> PCOutputs:
+                      seqack: bool = True) -> PCOutputs:
         import torch
 
         dev = torch.device("cuda", self.device)
@@ -525,7 +526,7 @@ class PacketContinue:
             conn=u8(L.rtn_out_conn_bytes(n)) if conn else None,
             conn_dlv=u8(L.rtn_out_conn_dlv_bytes(n, self.conn_words)) if conn and self.conn_words else None,
             conn_words=self.conn_words if conn else 0,
-            tcp4=u8(L.rtn_out_tcp4_bytes(n)) if tcp4 else None,
+            seqack=u8(L.rtn_out_seqack_bytes(n)) if seqack else None,
         )
 
     def run(self, slab, stride: int, data_len, n: int | None = None, out: PCOutputs | None = None,
@@ -658,7 +659,7 @@ class MappedHost:
 def _out_struct(out: PCOutputs) -> _Out:
     ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
     return _Out(ptr(out.pc_bitmap), ptr(out.fwd_bitmap), ptr(out.l4), ptr(out.addr6), ptr(out.dlv_bitmap),
-                ptr(out.dlv_records), ptr(out.counters), ptr(out.conn), ptr(out.conn_dlv), ptr(out.tcp4))
+                ptr(out.dlv_records), ptr(out.counters), ptr(out.conn), ptr(out.conn_dlv), ptr(out.seqack))
 
 
 class _CtStats(C.Structure):

@@ -80,8 +80,8 @@ def test_output_sizes():
     assert CF == 256
     assert L.rtn_out_l4_bytes(65) == CF * 16
     assert L.rtn_out_l4_bytes(1025) == 1280 * 16
-    assert L.rtn_out_tcp4_bytes(1025) == 1280 * 8
-    assert L.rtn_out_addr6_bytes(1) == CF * 32
+    assert L.rtn_out_seqack_bytes(1025) == 1280 * 8
+    assert L.rtn_out_addr6_bytes(1) == CF * 24  # source bytes 8..15 + destination (bytes 0..7 in the record)
     assert L.rtn_out_dlv_bytes(64, 2) == CF * 2 * 8      # masks only: the frame is the rank in dlv_bitmap
     assert L.rtn_out_bitmap_bytes(0xFFFFFFFF) == ((1 << 32) // 64) * 8   # 64-bit arithmetic, no wrap
     assert L.rtn_out_l4_bytes(0xFFFFFFFF) == (1 << 32) * 16

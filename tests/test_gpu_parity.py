@@ -251,7 +251,7 @@ def test_large_tree_uses_nested_form_and_matches(gpu):
 
 
 def test_misaligned_record_array_is_einval(gpu):
-    """l4 / addr6 / conn / tcp4 take 16-B-per-lane stores: a misaligned array is refused
+    """l4 / addr6 / conn / seqack take 16-B-per-lane stores: a misaligned array is refused
     (RTN_EINVAL) before anything is launched, and the same context still runs on aligned outputs."""
     import dataclasses
 
@@ -262,7 +262,7 @@ def test_misaligned_record_array_is_einval(gpu):
     d_slab = torch.from_numpy(slab).cuda()
     d_dlen = torch.from_numpy(dlen.view(np.int16)).cuda()
     out = ctx.alloc_outputs(len(dlen), conn=True)
-    for field in ("l4", "addr6", "conn", "tcp4"):
+    for field in ("l4", "addr6", "conn", "seqack"):
         t = getattr(out, field)
         bad = dataclasses.replace(out, **{field: torch.empty(t.numel() + 16, dtype=torch.uint8, device="cuda")[8:]})
         with pytest.raises(pc.RetinaError) as e:

@@ -210,17 +210,17 @@ VARIANTS.update({"withconn": withconn})
 
 
 def not4(src: str) -> str:
-    """Timing only: no IPv4-TCP seq/ack side stream (the tcp4 ring and its stores)."""
-    return _sub(src, "const bool t4 = fwd && v.v4 && v.tcp && (a.flags & 32u);", "const bool t4 = false;")
+    """Timing only: no TCP seq/ack side stream (the seqack ring and its stores)."""
+    return _sub(src, "const bool t4 = fwd && v.tcp && (a.flags & 32u);", "const bool t4 = false;")
 
 
 def pad128(src: str) -> str:
     """Chunk-end stores padded to whole 128-B lines (the round-2 form) instead of 64-B requests:
-    records to 8, seq/ack entries to 16, IPv6 address records to 4. (As pad64 against the 128-B
+    records to 8, seq/ack entries to 16, IPv6 address bytes to 128. (As pad64 against the 128-B
     form, in-process on one box: cfg4 0.1671 -> 0.1655 ms, cfg3 and cfg2 unchanged.)"""
     src = _sub(src, "  const rtn_u32 nl = (nrecs + 3u) & ~3u;", "  const rtn_u32 nl = (nrecs + 7u) & ~7u;")
     src = _sub(src, "  const rtn_u32 nl = ((nent + 1u) / 2u + 3u) & ~3u;", "  const rtn_u32 nl = ((nent + 1u) / 2u + 7u) & ~7u;")
-    return _sub(src, "  const rtn_u32 nv4 = ((nent + 1u) & ~1u) * 2u;", "  const rtn_u32 nv4 = ((nent + 3u) & ~3u) * 2u;")
+    return _sub(src, "  const rtn_u32 nu = ((nent * 24u + 63u) & ~63u) / 16u;", "  const rtn_u32 nu = ((nent * 24u + 127u) & ~127u) / 16u;")
 
 
 def noq6(src: str) -> str:
@@ -231,10 +231,10 @@ def noq6(src: str) -> str:
 
 
 def t4dense(src: str) -> str:
-    """Timing only: a chunk's seq/ack entries dense per chunk (chunk * 256 + IPv4-TCP rank, like
+    """Timing only: a chunk's seq/ack entries dense per chunk (chunk * 256 + TCP rank, like
     addr6) instead of in RTN_REC_INDEX blocks: one contiguous run per chunk."""
     return _sub(src, "  if (lane < nl) RTN_ST(dst + (lane / (RTN_RB / 2u)) * nch * (RTN_RB / 2u) + lane % (RTN_RB / 2u), src[lane]);\n}\n\n// IPv6",
-                "  (void)dst;\n  rtn_v4u* dd = reinterpret_cast<rtn_v4u*>(a.tcp4 + ch.rec_base + ch.ntflushed);\n"
+                "  (void)dst;\n  rtn_v4u* dd = reinterpret_cast<rtn_v4u*>(a.seqack + ch.rec_base + ch.ntflushed);\n"
                 "  if (lane < nl) RTN_ST(dd + lane, src[lane]);\n}\n\n// IPv6")
 
 
@@ -262,15 +262,9 @@ def ksb(src: str) -> str:
     return _sub(src, "#ifndef RTN_K\n", "#define RTN_K(c) (__builtin_amdgcn_sched_barrier(0), (c))\n#ifndef RTN_K\n")
 
 
-def ring6mod(src: str) -> str:
-    """The IPv6 ring indexed with a modulo (the round-2 form) instead of rtn_ring6_at."""
-    src = _sub(src, "ring6[rtn_ring6_at(ch.nv6flushed % RTN_RING6 + k / 2u) * 2u + (k & 1u)]",
-               "ring6[((ch.nv6flushed + k / 2u) % RTN_RING6) * 2u + (k & 1u)]")
-    return _sub(src, "const rtn_u32 at = rtn_ring6_at(ch.nv6 % RTN_RING6 + rank6);", "const rtn_u32 at = (ch.nv6 + rank6) % RTN_RING6;")
-
 
 VARIANTS.update({"not4": not4, "pad128": pad128, "noq6": noq6, "t4dense": t4dense, "recdense": recdense,
-                 "dmsb": dmsb, "ksb": ksb, "ring6mod": ring6mod})
+                 "dmsb": dmsb, "ksb": ksb})
 
 
 def nodlv(src: str) -> str:
