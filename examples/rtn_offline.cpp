@@ -32,6 +32,7 @@
 #include <vector>
 
 #include "retina_ct.h"
+#include "retina_stage.h"
 #include "retina_ingest.h"
 #include "retina_pc.h"
 
@@ -143,14 +144,15 @@ void walk(const HostSet& h, bool with_ct, Totals& t, FILE* dump) {
 int main(int argc, char** argv) {
   if (argc < 3) {
     fprintf(stderr, "usage: rtn_offline <spec.toml> <capture> [--batch N] [--mtu M] [--device D] [--no-ct] "
-                    "[--ct-log2 L] [--max-conn C] [--dump FILE] [--layout compact|mono]\n");
+                    "[--ct-log2 L] [--max-conn C] [--dump FILE] [--layout compact|mono|gpu] [--window BYTES]\n");
     return 2;
   }
   uint32_t batch = 1u << 20, mtu = 9702, ct_log2 = 24, max_conn = 10000000;  // configs/offline.toml
   int device = 0;
   bool with_ct = true;
   const char* dump_path = nullptr;
-  bool compact = true;
+  bool compact = true, gpu_walk = false;  // gpu: the capture walk on the GPU (rtn_pcap_next_batch_gpu)
+  uint64_t window = 0;
   for (int a = 3; a < argc; ++a) {
     std::string s = argv[a];
     auto next = [&]() { return a + 1 < argc ? argv[++a] : (die("missing argument value", -22), nullptr); };
@@ -163,9 +165,11 @@ int main(int argc, char** argv) {
     else if (s == "--dump") dump_path = next();
     else if (s == "--layout") {
       const std::string l = next();
-      if (l != "compact" && l != "mono") die("--layout compact|mono", -22);
-      compact = l == "compact";
+      if (l != "compact" && l != "mono" && l != "gpu") die("--layout compact|mono|gpu", -22);
+      compact = l != "mono";
+      gpu_walk = l == "gpu";
     }
+    else if (s == "--window") window = strtoull(next(), nullptr, 10);
     else die(("unknown option " + s).c_str(), -22);
   }
   batch = (batch + RTN_CHUNK_FRAMES - 1) / RTN_CHUNK_FRAMES * RTN_CHUNK_FRAMES;
@@ -186,6 +190,7 @@ int main(int argc, char** argv) {
   if (with_ct) RTN_CHECK(rtn_ct_create(device, ct_log2, max_conn, &ct));
   rtn_pcap_t* cap = nullptr;
   RTN_CHECK(rtn_pcap_open(argv[2], mtu, &cap));
+  if (window) RTN_CHECK(rtn_pcap_gpu_window(cap, window));
   FILE* dump = dump_path ? fopen(dump_path, "w") : nullptr;
 
   // device buffers (one set: the stream orders the batches)
@@ -247,10 +252,14 @@ int main(int argc, char** argv) {
     }
     uint32_t n = 0;
     const auto tp = now();
-    if (compact)
+    if (gpu_walk) {  // the file's bytes to HBM, records found and frames packed by the GPU
+      rtn_stage_slab_t sl = {d_slab, d_ext, d_chunk, d_dlen, batch, batch};
+      RTN_CHECK(rtn_pcap_next_batch_gpu(cap, device, &sl, &n, stream));
+    } else if (compact) {
       RTN_CHECK(rtn_pcap_next_batch_split(cap, h.slab, h.ext, batch, h.ext_chunk, h.dlen, batch, &n, &h.rows));
-    else
+    } else {
       RTN_CHECK(rtn_pcap_next_batch(cap, h.slab, kStride, h.dlen, batch, &n));
+    }
     t_pack += secs_since(tp);
     if (n == 0) break;
     h.n = n;
@@ -258,10 +267,17 @@ int main(int argc, char** argv) {
     next_frame += n;
     t.frames += n;
     const size_t nbm = rtn_out_bitmap_bytes(n);
-    HIP_CHECK(hipMemcpyAsync(d_slab, h.slab, (size_t)n * stride, hipMemcpyHostToDevice, stream));
-    HIP_CHECK(hipMemcpyAsync(d_dlen, h.dlen, (size_t)n * 2u, hipMemcpyHostToDevice, stream));
     rtn_batch_t b = {d_slab, stride, d_dlen, n, 0u, nullptr, 0u, 0u, nullptr};
-    if (compact) {
+    if (gpu_walk) {
+      b.ext = d_ext;
+      b.ext_rows = rtn_stage_gather_ext_rows(n);
+      b.ext_chunk = d_chunk;
+      b.flags = RTN_BATCH_EXT_COMPACT;
+    } else {
+      HIP_CHECK(hipMemcpyAsync(d_slab, h.slab, (size_t)n * stride, hipMemcpyHostToDevice, stream));
+      HIP_CHECK(hipMemcpyAsync(d_dlen, h.dlen, (size_t)n * 2u, hipMemcpyHostToDevice, stream));
+    }
+    if (compact && !gpu_walk) {
       if (h.rows) HIP_CHECK(hipMemcpyAsync(d_ext, h.ext, (size_t)h.rows * 64u, hipMemcpyHostToDevice, stream));
       HIP_CHECK(hipMemcpyAsync(d_chunk, h.ext_chunk, ((n + RTN_CHUNK_FRAMES - 1) / RTN_CHUNK_FRAMES) * 4u,
                                hipMemcpyHostToDevice, stream));
@@ -304,7 +320,8 @@ int main(int argc, char** argv) {
          (unsigned long long)ps.bytes, (unsigned long long)t.pc, (unsigned long long)t.fwd, (unsigned long long)t.tcp,
          (unsigned long long)t.udp, (unsigned long long)t.status[1], (unsigned long long)t.status[2],
          (unsigned long long)t.status[3], (unsigned long long)t.status[4], (unsigned long long)t.status[5],
-         (unsigned long long)t.status[6], (unsigned long long)t.prior, cs.live, secs, t.frames / secs / 1e6, batch, compact ? "compact" : "mono", t_pack, t_wait,
+         (unsigned long long)t.status[6], (unsigned long long)t.prior, cs.live, secs, t.frames / secs / 1e6, batch,
+         gpu_walk ? "gpu" : (compact ? "compact" : "mono"), t_pack, t_wait,
          t_walk);
   if (dump) fclose(dump);
   rtn_pcap_close(cap);

@@ -46,6 +46,24 @@ int32_t rtn_pcap_next_batch(rtn_pcap_t* p, uint8_t* slab, uint64_t stride, uint1
  * fails with RTN_ERANGE (*n = 0), so that *n == 0 with RTN_OK always means end of file. */
 int32_t rtn_pcap_next_batch_split(rtn_pcap_t* p, uint8_t* head, uint8_t* ext, uint32_t ext_cap, uint32_t* ext_chunk,
                                   uint16_t* data_len, uint32_t cap, uint32_t* n, uint32_t* rows);
+/* The same frames with the capture walk on the GPU (the host copies the file's bytes, the device
+ * finds the records): a window of the capture (rtn_pcap_gpu_window, default 256 MiB) is copied to
+ * HBM as it is, and gfx950 kernels find its record chain in parallel (speculated per 4-KiB
+ * segment, then confirmed exactly from the window's first record), apply the offline runtime's
+ * rules (mtu skip, data_len = captured bytes) and pack up to slab->cap kept frames into `slab`,
+ * in device memory, in the gather layout of rtn_stage_gather (retina_stage.h: head slots, ext
+ * rows compact within each chunk at rows [c * RTN_CHUNK_FRAMES, ...), ext_chunk[c] =
+ * c * RTN_CHUNK_FRAMES; slab->ext_cap >= rtn_stage_gather_ext_rows(slab->cap)). The packing is
+ * left running on `stream` (a hipStream_t; use one stream per capture); *n, the stats and the
+ * file position are final on return. *n == 0 with RTN_OK means end of file. A kept frame longer
+ * than 65535 bytes ends the batch before it with RTN_ERANGE (as rtn_pcap_next_batch); pcapng
+ * sections in different byte orders are refused (RTN_EINVAL). Calls may be mixed with the host
+ * readers above: they share the file position and the stats. */
+struct rtn_stage_slab;
+int32_t rtn_pcap_next_batch_gpu(rtn_pcap_t* p, int device, const struct rtn_stage_slab* slab, uint32_t* n,
+                                void* stream);
+/* Window size of rtn_pcap_next_batch_gpu in bytes (64 KiB .. 1 TiB); every record must fit in one. */
+int32_t rtn_pcap_gpu_window(rtn_pcap_t* p, uint64_t bytes);
 int32_t rtn_pcap_stats(const rtn_pcap_t* p, rtn_pcap_stats_t* st);
 /* Start again from the first frame (stats are kept). */
 int32_t rtn_pcap_rewind(rtn_pcap_t* p);

@@ -52,10 +52,11 @@ def build_library(force: bool = False) -> Path:
     inc = _gen_kernel_inc()
     inc_ct = _gen_kernel_inc("ct_kernel", "kCtKernelSrc")
     inc_st = _gen_kernel_inc("stage_kernel", "kStageKernelSrc", "ingest")
+    inc_cw = _gen_kernel_inc("capwalk_kernel", "kCapwalkKernelSrc", "ingest")
     fg = [CSRC / "filtergen" / s for s in FILTERGEN_SRCS]
     rt = [CSRC / s for s in RUNTIME_SRCS]
     hdrs = (list((CSRC / "filtergen").glob("*.hpp")) + list((CSRC / "runtime").glob("*.hpp"))
-            + list((ROOT / "include").glob("*.h")) + [inc, inc_ct, inc_st])
+            + list((ROOT / "include").glob("*.h")) + [inc, inc_ct, inc_st, inc_cw])
     so = LIB / SO_NAME
     if force or _stale(so, fg + rt + hdrs):
         cmd = [
@@ -96,6 +97,12 @@ def build_kernel_check() -> Path:
     if _stale(st_out, [st_src]):
         _run([str(ROCM / "bin" / "hipcc"), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "--genco",
               str(st_src), "-o", str(st_out)])
+    # ... and the capture-walk kernels (rtn_pcap_next_batch_gpu)
+    cw_src = CSRC / "kernels" / "capwalk_kernel.hip"
+    cw_out = LIB / "capwalk_kernel.hsaco"
+    if _stale(cw_out, [cw_src]):
+        _run([str(ROCM / "bin" / "hipcc"), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "--genco",
+              str(cw_src), "-o", str(cw_out)])
     out = LIB / "pc_kernel_cfg2.hsaco"
     src = LIB / "pc_kernel_cfg2.hip"
     tpl = CSRC / "kernels" / "pc_kernel.hip"

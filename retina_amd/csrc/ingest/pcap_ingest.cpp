@@ -5,16 +5,27 @@
 // walked once; packing is a bounded memcpy per frame.
 #include "retina_ingest.h"
 
+#include <hip/hip_runtime.h>
 #include <fcntl.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cstring>
+#include <memory>
 #include <string>
+#include <thread>
+#include <vector>
 
 #include "../runtime/rtn_error.hpp"
 #include "retina_pc.h"
+#include "retina_stage.h"
+
+namespace rtn_gpu_walk {
+struct State;
+void destroy(State* g);
+}  // namespace rtn_gpu_walk
 
 namespace {
 
@@ -44,6 +55,7 @@ struct rtn_pcap {
   rtn_pcap_stats_t st{};
   size_t populated = 0;  // page tables mapped up to here (prefault)
   size_t prefetched = 0; // cache lines requested up to here (prefetch_ahead)
+  rtn_gpu_walk::State* gpu = nullptr;  // rtn_pcap_next_batch_gpu's device state
 };
 
 namespace {
@@ -269,8 +281,345 @@ int32_t rtn_pcap_rewind(rtn_pcap_t* p) {
 
 void rtn_pcap_close(rtn_pcap_t* p) {
   if (!p) return;
+  rtn_gpu_walk::destroy(p->gpu);
   if (p->base) munmap(const_cast<uint8_t*>(p->base), p->size);
   delete p;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------------------------
+// rtn_pcap_next_batch_gpu: the capture walk on the GPU (csrc/kernels/capwalk_kernel.hip). A window
+// of the file, starting at a record, is copied to HBM as it is (worker threads copy the mapped
+// file into pinned memory, then one host -> HBM copy); the kernels find the window's record
+// chain, apply the offline runtime's rules and pack the kept frames into the gather layout of
+// rtn_stage_gather; the window stays resident, so a batch cut short by `cap` continues from it.
+namespace rtn_gpu_walk {
+#include "capwalk_kernel_src.inc"  // kCapwalkKernelSrc
+
+constexpr uint64_t kSeg = 4096;  // RTN_CAP_SEG
+constexpr uint32_t kCand = 8;    // RTN_CAP_C
+constexpr uint64_t kStop = 1ull << 63, kEof = 1ull << 61, kErr = 1ull << 60, kDead = 1ull << 59;
+constexpr uint64_t kOffMask = 0xFFFFFFFFFFFFull;
+constexpr uint64_t kPad = 256;  // readable bytes past a window (unaligned word reads, ext rows)
+
+struct CapArgs {  // rtn_cap_args
+  const uint8_t* win;
+  uint64_t bytes;
+  uint32_t nseg, fmt, swap, mtu, at_eof, levels, k, pad0;
+  uint64_t* cand;
+  uint32_t* ncand;
+  uint64_t* nexit;
+  uint32_t* ncnt;
+  uint32_t* jump;
+  uint32_t* path;
+  uint32_t* pre;
+  uint32_t* red;
+  uint32_t* tgt;
+  uint32_t cap, pad1;
+  uint64_t* ptrs;
+  uint16_t* dlen;
+  uint64_t* cut;
+};
+struct PackArgs {  // rtn_cap_pack_args
+  const uint64_t* ptrs;
+  const uint16_t* dl;
+  uint8_t* head;
+  uint8_t* ext;
+  uint32_t* ext_chunk;
+  uint16_t* dlen;
+  uint32_t n;
+};
+struct Res {  // device result block, copied back once per window
+  uint64_t cut[4];
+  uint32_t red[4];
+  uint32_t tgt[2];
+};
+
+struct State {
+  int device = -1;
+  uint64_t window = 256ull << 20;
+  hipModule_t module = nullptr;
+  hipFunction_t cand = nullptr, nodes = nullptr, jump = nullptr, lift = nullptr, scan = nullptr, emit = nullptr,
+                pack = nullptr;
+  uint8_t* d_win = nullptr;  // window + kPad
+  uint64_t d_win_cap = 0;
+  uint8_t* h_stage = nullptr;  // pinned
+  uint64_t h_cap = 0;
+  uint8_t* d_seg = nullptr;  // per-segment / per-node arrays for seg_cap segments
+  uint32_t seg_cap = 0;
+  Res* d_res = nullptr;
+  Res* h_res = nullptr;
+  uint64_t* d_ptrs = nullptr;
+  uint16_t* d_dl = nullptr;
+  uint32_t list_cap = 0;
+  // the resident window: file bytes [win_off, win_off + win_len) at d_win
+  size_t win_off = 0, win_len = 0;
+  bool win_valid = false;
+};
+
+void destroy(State* g) {
+  if (!g) return;
+  if (g->device >= 0) (void)hipSetDevice(g->device);
+  if (g->d_win) (void)hipFree(g->d_win);
+  if (g->h_stage) (void)hipHostFree(g->h_stage);
+  if (g->d_seg) (void)hipFree(g->d_seg);
+  if (g->d_res) (void)hipFree(g->d_res);
+  if (g->h_res) (void)hipHostFree(g->h_res);
+  if (g->d_ptrs) (void)hipFree(g->d_ptrs);
+  if (g->d_dl) (void)hipFree(g->d_dl);
+  if (g->module) (void)hipModuleUnload(g->module);
+  delete g;
+}
+
+int32_t hip_fail(const char* what, hipError_t e) {
+  return rtn::set_error(RTN_EDEVICE, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+int32_t init(State* g, int device) {
+  hipError_t e = hipSetDevice(device);
+  if (e != hipSuccess) return hip_fail("hipSetDevice", e);
+  std::shared_ptr<std::vector<uint8_t>> code;
+  int32_t rc = rtn::compile_hip(kCapwalkKernelSrc, code);
+  if (rc) return rc;
+  e = hipModuleLoadData(&g->module, code->data());
+  if (e != hipSuccess) return hip_fail("hipModuleLoadData", e);
+  const char* names[] = {"rtn_cap_cand", "rtn_cap_nodes", "rtn_cap_jump", "rtn_cap_lift", "rtn_cap_scan", "rtn_cap_emit",
+                         "rtn_cap_pack"};
+  hipFunction_t* fns[] = {&g->cand, &g->nodes, &g->jump, &g->lift, &g->scan, &g->emit, &g->pack};
+  for (int k = 0; k < 7; ++k) {
+    e = hipModuleGetFunction(fns[k], g->module, names[k]);
+    if (e != hipSuccess) return hip_fail("hipModuleGetFunction", e);
+  }
+  e = hipMalloc(reinterpret_cast<void**>(&g->d_res), sizeof(Res));
+  if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&g->h_res), sizeof(Res), hipHostMallocDefault);
+  if (e != hipSuccess) return hip_fail("rtn_pcap_next_batch_gpu: result block", e);
+  g->device = device;
+  return RTN_OK;
+}
+
+// Pointer-jumping levels for nseg segments: the chain has at most nseg nodes.
+uint32_t levels(uint32_t nseg) {
+  uint32_t k = 1;
+  while ((1ull << k) < (uint64_t)nseg + 1) ++k;
+  return k;
+}
+// The per-segment arrays in one allocation, laid out by carve().
+size_t seg_bytes(uint32_t nseg) {
+  const size_t nodes = (size_t)nseg * kCand;
+  return nodes * 8 + (size_t)nseg * 4 + nodes * 8 + nodes * 12 + (levels(nseg) + 1) * nodes * 4 + (size_t)nseg * 4 +
+         (size_t)nseg * 8 + 64;
+}
+void carve(uint8_t* q, uint32_t nseg_cap, CapArgs& a) {
+  const size_t nodes = (size_t)nseg_cap * kCand;
+  a.cand = reinterpret_cast<uint64_t*>(q);
+  q += nodes * 8;
+  a.nexit = reinterpret_cast<uint64_t*>(q);
+  q += nodes * 8;
+  a.ncand = reinterpret_cast<uint32_t*>(q);
+  q += (size_t)nseg_cap * 4;
+  a.ncnt = reinterpret_cast<uint32_t*>(q);
+  q += nodes * 12;
+  a.path = reinterpret_cast<uint32_t*>(q);
+  q += (size_t)nseg_cap * 4;
+  a.pre = reinterpret_cast<uint32_t*>(q);
+  q += (size_t)nseg_cap * 8;
+  a.jump = reinterpret_cast<uint32_t*>(q);  // [levels + 1][nseg * kCand] of the current window
+}
+
+// Buffers for a window of `bytes` and a batch of `cap` frames (grown, never shrunk).
+int32_t reserve(State* g, uint64_t bytes, uint32_t cap) {
+  hipError_t e = hipSuccess;
+  if (bytes + kPad > g->d_win_cap) {
+    if (g->d_win) (void)hipFree(g->d_win);
+    g->d_win = nullptr;
+    e = hipMalloc(reinterpret_cast<void**>(&g->d_win), bytes + kPad);
+    if (e != hipSuccess) return hip_fail("hipMalloc (window)", e);
+    g->d_win_cap = bytes + kPad;
+    g->win_valid = false;
+  }
+  if (bytes > g->h_cap) {
+    if (g->h_stage) (void)hipHostFree(g->h_stage);
+    g->h_stage = nullptr;
+    e = hipHostMalloc(reinterpret_cast<void**>(&g->h_stage), bytes, hipHostMallocDefault);
+    if (e != hipSuccess) return hip_fail("hipHostMalloc (window)", e);
+    g->h_cap = bytes;
+  }
+  const uint32_t nseg = (uint32_t)((bytes + kSeg - 1) / kSeg);
+  if (nseg > g->seg_cap) {
+    if (g->d_seg) (void)hipFree(g->d_seg);
+    g->d_seg = nullptr;
+    e = hipMalloc(reinterpret_cast<void**>(&g->d_seg), seg_bytes(nseg));
+    if (e != hipSuccess) return hip_fail("hipMalloc (segments)", e);
+    g->seg_cap = nseg;
+  }
+  if (cap > g->list_cap) {
+    if (g->d_ptrs) (void)hipFree(g->d_ptrs);
+    if (g->d_dl) (void)hipFree(g->d_dl);
+    g->d_ptrs = nullptr;
+    g->d_dl = nullptr;
+    e = hipMalloc(reinterpret_cast<void**>(&g->d_ptrs), (size_t)cap * 8);
+    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&g->d_dl), (size_t)cap * 2);
+    if (e != hipSuccess) return hip_fail("hipMalloc (frame list)", e);
+    g->list_cap = cap;
+  }
+  return RTN_OK;
+}
+
+// file bytes [off, off + len) -> pinned staging, on worker threads (the first touch of each page
+// of the mapping is read from the page cache here)
+void copy_in(const uint8_t* src, uint8_t* dst, size_t len) {
+  const unsigned hw = std::thread::hardware_concurrency();
+  const size_t parts = std::min<size_t>(std::max(1u, std::min(hw, 8u)), std::max<size_t>(1, len >> 22));
+  if (parts <= 1) {
+    memcpy(dst, src, len);
+    return;
+  }
+  const size_t step = ((len + parts - 1) / parts + 63) & ~size_t(63);
+  std::vector<std::thread> th;
+  for (size_t k = 0; k < parts; ++k) {
+    const size_t a = k * step, b = std::min(len, a + step);
+    if (a >= b) break;
+    th.emplace_back([=] { memcpy(dst + a, src + a, b - a); });
+  }
+  for (auto& t : th) t.join();
+}
+}  // namespace rtn_gpu_walk
+
+extern "C" {
+
+int32_t rtn_pcap_gpu_window(rtn_pcap_t* p, uint64_t bytes) {
+  if (!p) return rtn::set_error(RTN_EINVAL, "null argument");
+  if (bytes < (1u << 16) || bytes > (1ull << 40)) return rtn::set_error(RTN_EINVAL, "window of 64 KiB .. 1 TiB");
+  if (!p->gpu) p->gpu = new rtn_gpu_walk::State();
+  p->gpu->window = bytes;
+  p->gpu->win_valid = false;
+  return RTN_OK;
+}
+
+int32_t rtn_pcap_next_batch_gpu(rtn_pcap_t* p, int device, const rtn_stage_slab_t* slab, uint32_t* n, void* stream) {
+  using namespace rtn_gpu_walk;
+  if (!p || !slab || !n) return rtn::set_error(RTN_EINVAL, "null argument");
+  *n = 0;
+  if (!slab->head || !slab->ext || !slab->ext_chunk || !slab->data_len || slab->cap == 0)
+    return rtn::set_error(RTN_EINVAL, "null argument");
+  if (slab->cap > RTN_MAX_FRAMES) return rtn::set_error(RTN_EINVAL, "cap larger than RTN_MAX_FRAMES");
+  if (slab->ext_cap < rtn_stage_gather_ext_rows(slab->cap))
+    return rtn::set_error(RTN_ERANGE, "the gather layout needs rtn_stage_gather_ext_rows(cap) ext rows");
+  if (((reinterpret_cast<uintptr_t>(slab->head) | reinterpret_cast<uintptr_t>(slab->ext)) & 15u) != 0)
+    return rtn::set_error(RTN_EINVAL, "head and ext must be 16-byte aligned");
+  if (!p->gpu) p->gpu = new State();
+  State* g = p->gpu;
+  if (g->device != device) {
+    if (g->device >= 0) return rtn::set_error(RTN_EINVAL, "a capture walks on one device");
+    int32_t rc = init(g, device);
+    if (rc) return rc;
+  }
+  hipError_t e = hipSetDevice(device);
+  if (e != hipSuccess) return hip_fail("hipSetDevice", e);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  // pcapng: the section's byte order, from the first section header when walking from the start
+  if (p->fmt == Fmt::Pcapng && p->off == p->first && p->size >= 12) {
+    uint32_t bom;
+    memcpy(&bom, p->base + 8, 4);
+    p->swap = bom != 0x1A2B3C4Du;
+  }
+  const bool swap = p->swap;
+  for (;;) {
+    if (p->off >= p->size) return RTN_OK;  // end of file: *n = 0
+    // the window: the resident one if this batch starts inside it with at least half of it (or
+    // the rest of the file) left, otherwise a fresh copy from here
+    const uint64_t want = std::min<uint64_t>(g->window, p->size - p->off);
+    int32_t rc = reserve(g, std::min<uint64_t>(g->window, p->size - p->first), slab->cap);
+    if (rc) return rc;
+    bool fresh = !(g->win_valid && p->off >= g->win_off && p->off < g->win_off + g->win_len);
+    if (!fresh) {
+      const uint64_t left = g->win_off + g->win_len - p->off;
+      fresh = left < g->window / 2 && g->win_off + g->win_len < p->size;
+    }
+    if (fresh) {
+      prefault(p, p->off, want);
+      e = hipStreamSynchronize(s);  // the staging buffer's previous copy has left
+      if (e != hipSuccess) return hip_fail("hipStreamSynchronize", e);
+      copy_in(p->base + p->off, g->h_stage, want);
+      e = hipMemcpyAsync(g->d_win, g->h_stage, want, hipMemcpyHostToDevice, s);
+      if (e == hipSuccess) e = hipMemsetAsync(g->d_win + want, 0, kPad, s);
+      if (e != hipSuccess) return hip_fail("window copy", e);
+      g->win_off = p->off;
+      g->win_len = want;
+      g->win_valid = true;
+    }
+    const uint64_t rel = p->off - g->win_off, bytes = g->win_len - rel;
+    const bool at_eof = g->win_off + g->win_len == p->size;
+    CapArgs a{};
+    a.win = g->d_win + rel;
+    a.bytes = bytes;
+    a.nseg = (uint32_t)((bytes + kSeg - 1) / kSeg);
+    a.fmt = p->fmt == Fmt::Pcapng ? 1u : 0u;
+    a.swap = swap ? 1u : 0u;
+    a.mtu = p->mtu;
+    a.at_eof = at_eof ? 1u : 0u;
+    carve(g->d_seg, g->seg_cap, a);
+    a.levels = levels(a.nseg);
+    a.red = g->d_res->red;
+    a.tgt = g->d_res->tgt;
+    a.cut = g->d_res->cut;
+    a.cap = slab->cap;
+    a.ptrs = g->d_ptrs;
+    a.dlen = g->d_dl;
+    void* params[] = {&a};
+    e = hipMemsetAsync(g->d_res, 0, sizeof(Res), s);
+    const uint32_t nb4 = (a.nseg + 3) / 4, nb256 = (a.nseg + 255) / 256, nbn = (a.nseg * kCand + 255) / 256;
+    if (e == hipSuccess) e = hipModuleLaunchKernel(g->cand, nb4, 1, 1, 256, 1, 1, 0, s, params, nullptr);
+    if (e == hipSuccess) e = hipModuleLaunchKernel(g->nodes, nbn, 1, 1, 256, 1, 1, 0, s, params, nullptr);
+    for (uint32_t k = 1; k <= a.levels && e == hipSuccess; ++k) {
+      a.k = k;  // (the launch copies the arguments)
+      e = hipModuleLaunchKernel(g->jump, nbn, 1, 1, 256, 1, 1, 0, s, params, nullptr);
+    }
+    if (e == hipSuccess) e = hipModuleLaunchKernel(g->lift, nb256, 1, 1, 256, 1, 1, 0, s, params, nullptr);
+    if (e == hipSuccess) e = hipModuleLaunchKernel(g->scan, 1, 1, 1, 1024, 1, 1, 0, s, params, nullptr);
+    if (e == hipSuccess) e = hipModuleLaunchKernel(g->emit, nb256, 1, 1, 256, 1, 1, 0, s, params, nullptr);
+    if (e == hipSuccess) e = hipMemcpyAsync(g->h_res, g->d_res, sizeof(Res), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return hip_fail("rtn_pcap_next_batch_gpu", e);
+    const Res r = *g->h_res;
+    const uint32_t recs = r.red[2], kept = r.red[3], tgt = r.tgt[0], bad = r.tgt[1];
+    const uint64_t ex = r.cut[2];
+    if ((ex & kStop) && (ex & kErr) && tgt == kept)
+      return rtn::set_error(RTN_EINVAL, "pcapng sections in different byte orders: use rtn_pcap_next_batch_split");
+    if (tgt < kept) {  // cut by cap or by a frame longer than 65535 bytes
+      p->off += r.cut[0];
+      p->st.frames += r.cut[1];
+      p->st.skipped_mtu += r.cut[1] - tgt;
+    } else {
+      p->st.frames += recs;
+      p->st.skipped_mtu += recs - kept;
+      if (ex & kDead) {  // the chain reached a record no candidate matched: the next batch starts there
+        p->off += ex & kOffMask;
+      } else if (!(ex & kStop)) {
+        p->off += bytes;
+      } else if ((ex & kEof) || at_eof) {
+        p->off = p->size;  // the capture ends here, as the host reader ends
+      } else if ((ex & kOffMask) == 0) {
+        return rtn::set_error(RTN_ERANGE, "a record larger than the GPU window (rtn_pcap_gpu_window)");
+      } else {
+        p->off += ex & kOffMask;
+      }
+    }
+    p->st.packed += tgt;
+    p->st.bytes += r.cut[3];
+    if (tgt > 0) {
+      PackArgs pa{g->d_ptrs, g->d_dl, slab->head, slab->ext, slab->ext_chunk, slab->data_len, tgt};
+      void* pp[] = {&pa};
+      const uint32_t chunks = (tgt + RTN_CHUNK_FRAMES - 1) / RTN_CHUNK_FRAMES;
+      e = hipModuleLaunchKernel(g->pack, (chunks + 3) / 4, 1, 1, 256, 1, 1, 0, s, pp, nullptr);
+      if (e != hipSuccess) return hip_fail("rtn_cap_pack", e);
+      *n = tgt;
+    }
+    if (bad == tgt && bad < kept) return rtn::set_error(RTN_ERANGE, "captured frame longer than 65535 bytes");
+    if (tgt > 0) return RTN_OK;
+    // every frame of the window was skipped: go on with the next one
+  }
 }
 
 }  // extern "C"

@@ -139,6 +139,9 @@ EXPORTS = {
     "rtn_pcap_next_batch_split": (C.c_int32, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p,
                                               C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
     "rtn_pcap_stats": (C.c_int32, [C.c_void_p, C.POINTER(_PcapStats)]),
+    "rtn_pcap_next_batch_gpu": (C.c_int32, [C.c_void_p, C.c_int, C.POINTER(_StageSlab), C.POINTER(C.c_uint32),
+                                            C.c_void_p]),
+    "rtn_pcap_gpu_window": (C.c_int32, [C.c_void_p, C.c_uint64]),
     "rtn_pcap_rewind": (C.c_int32, [C.c_void_p]),
     "rtn_pcap_close": (None, [C.c_void_p]),
     # include/retina_stage.h
@@ -808,6 +811,23 @@ class PcapReader:
                                                ext_chunk.ctypes.data, data_len.ctypes.data, cap, C.byref(n),
                                                C.byref(rows)))
         return n.value, rows.value
+
+    def next_batch_gpu(self, head, ext, ext_chunk, dlen_out, device: int = 0, stream=None) -> int:
+        """rtn_pcap_next_batch_gpu: the capture walk on the GPU into device tensors in the gather
+        layout (head: uint8 cap*64, ext: uint8 >= gather_ext_rows(cap)*64, ext_chunk: int32/uint32
+        ceil(cap/CHUNK_FRAMES), dlen_out: int16/uint16 cap); returns the frames of the batch. The
+        packing runs on `stream` (default: the current torch stream)."""
+        import torch
+
+        cap = dlen_out.numel()
+        slab = _StageSlab(_addr(head), _addr(ext), _addr(ext_chunk), _addr(dlen_out), cap, ext.numel() // 64)
+        s = stream if stream is not None else torch.cuda.current_stream(device)
+        n = C.c_uint32()
+        _check(lib().rtn_pcap_next_batch_gpu(self._h, device, C.byref(slab), C.byref(n), s.cuda_stream))
+        return n.value
+
+    def gpu_window(self, nbytes: int) -> None:
+        _check(lib().rtn_pcap_gpu_window(self._h, nbytes))
 
     def rewind(self) -> None:
         _check(lib().rtn_pcap_rewind(self._h))

@@ -36,7 +36,7 @@ def test_offline_runtime_is_built():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("layout", ["compact", "mono"])
+@pytest.mark.parametrize("layout", ["compact", "mono", "gpu"])
 def test_offline_runtime_vs_oracle(gpu, tmp_path, layout):
     rng = np.random.default_rng(3)
     pool = helpers.flow_pool(rng, 700)
@@ -56,7 +56,8 @@ def test_offline_runtime_vs_oracle(gpu, tmp_path, layout):
     dump = tmp_path / "dump.txt"
     batch = 2048
     r = subprocess.run([str(EXE), str(spec), str(cap), "--batch", str(batch), "--mtu", "1500", "--ct-log2", "16",
-                        "--dump", str(dump), "--layout", layout], capture_output=True, text=True, timeout=120)
+                        "--dump", str(dump), "--layout", layout, "--window", str(1 << 16)],
+                       capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     summary = json.loads(r.stdout.strip().splitlines()[-1])
     assert summary["layout"] == layout

@@ -1,6 +1,7 @@
 """End-to-end offline runtime (examples/rtn_offline.cpp) on a synthetic capture: writes a libpcap
 file of full frames (the bench's seeded cfg2 or cfg3 frames, zero payload), then runs the C++
-offline runtime over it in each layout and prints its JSON summary lines.
+offline runtime over it in each layout (gpu: the capture walk on the GPU) and prints its JSON
+summary lines.
 
     python tools/offline_bench.py cfg2|cfg3 [frames] [--no-ct]
 """
@@ -57,7 +58,7 @@ def main() -> None:
         spec = Path(d) / "spec.toml"
         spec.write_text(bench.spec_for(cfg))
         exe = ROOT / "retina_amd" / "_lib" / "rtn_offline"
-        for layout in ("compact", "mono"):
+        for layout in ("gpu", "compact", "mono"):
             for _ in range(2):  # the second run has the capture in the page cache
                 r = subprocess.run([str(exe), str(spec), str(cap), "--layout", layout, *extra],
                                    capture_output=True, text=True, timeout=300)
