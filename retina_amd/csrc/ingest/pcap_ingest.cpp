@@ -356,6 +356,7 @@ struct State {
   // the resident window: file bytes [win_off, win_off + win_len) at d_win
   size_t win_off = 0, win_len = 0;
   bool win_valid = false;
+  uint64_t last_batch = 0;  // file bytes the last batch consumed
 };
 
 void destroy(State* g) {
@@ -470,7 +471,7 @@ int32_t reserve(State* g, uint64_t bytes, uint32_t cap) {
 // of the mapping is read from the page cache here)
 void copy_in(const uint8_t* src, uint8_t* dst, size_t len) {
   const unsigned hw = std::thread::hardware_concurrency();
-  const size_t parts = std::min<size_t>(std::max(1u, std::min(hw, 8u)), std::max<size_t>(1, len >> 22));
+  const size_t parts = std::min<size_t>(std::max(1u, std::min(hw, 8u)), std::max<size_t>(1, len >> 21));
   if (parts <= 1) {
     memcpy(dst, src, len);
     return;
@@ -533,16 +534,23 @@ int32_t rtn_pcap_next_batch_gpu(rtn_pcap_t* p, int device, const rtn_stage_slab_
     int32_t rc = reserve(g, std::min<uint64_t>(g->window, p->size - p->first), slab->cap);
     if (rc) return rc;
     bool fresh = !(g->win_valid && p->off >= g->win_off && p->off < g->win_off + g->win_len);
-    if (!fresh) {
+    if (!fresh) {  // the rest of the resident window, if it holds about a batch (the last one's bytes)
       const uint64_t left = g->win_off + g->win_len - p->off;
-      fresh = left < g->window / 2 && g->win_off + g->win_len < p->size;
+      fresh = left < std::max<uint64_t>(g->last_batch, 1u << 20) && g->win_off + g->win_len < p->size;
     }
+    const size_t off0 = p->off;
     if (fresh) {
       prefault(p, p->off, want);
       e = hipStreamSynchronize(s);  // the staging buffer's previous copy has left
       if (e != hipSuccess) return hip_fail("hipStreamSynchronize", e);
-      copy_in(p->base + p->off, g->h_stage, want);
-      e = hipMemcpyAsync(g->d_win, g->h_stage, want, hipMemcpyHostToDevice, s);
+      // 16-MiB pieces: the host copies piece k + 1 while the copy engine moves piece k
+      constexpr uint64_t kPiece = 16ull << 20;
+      e = hipSuccess;
+      for (uint64_t a0 = 0; a0 < want && e == hipSuccess; a0 += kPiece) {
+        const uint64_t len = std::min(kPiece, want - a0);
+        copy_in(p->base + p->off + a0, g->h_stage + a0, len);
+        e = hipMemcpyAsync(g->d_win + a0, g->h_stage + a0, len, hipMemcpyHostToDevice, s);
+      }
       if (e == hipSuccess) e = hipMemsetAsync(g->d_win + want, 0, kPad, s);
       if (e != hipSuccess) return hip_fail("window copy", e);
       g->win_off = p->off;
@@ -608,6 +616,7 @@ int32_t rtn_pcap_next_batch_gpu(rtn_pcap_t* p, int device, const rtn_stage_slab_
     }
     p->st.packed += tgt;
     p->st.bytes += r.cut[3];
+    g->last_batch = p->off - off0;
     if (tgt > 0) {
       PackArgs pa{g->d_ptrs, g->d_dl, slab->head, slab->ext, slab->ext_chunk, slab->data_len, tgt};
       void* pp[] = {&pa};
