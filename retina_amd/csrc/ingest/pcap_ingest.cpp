@@ -357,6 +357,7 @@ struct State {
   size_t win_off = 0, win_len = 0;
   bool win_valid = false;
   uint64_t last_batch = 0;  // file bytes the last batch consumed
+  hipEvent_t packed = nullptr;  // after the last batch's packing (it reads the window and frame list)
 };
 
 void destroy(State* g) {
@@ -369,6 +370,7 @@ void destroy(State* g) {
   if (g->h_res) (void)hipHostFree(g->h_res);
   if (g->d_ptrs) (void)hipFree(g->d_ptrs);
   if (g->d_dl) (void)hipFree(g->d_dl);
+  if (g->packed) (void)hipEventDestroy(g->packed);
   if (g->module) (void)hipModuleUnload(g->module);
   delete g;
 }
@@ -392,7 +394,8 @@ int32_t init(State* g, int device) {
     e = hipModuleGetFunction(fns[k], g->module, names[k]);
     if (e != hipSuccess) return hip_fail("hipModuleGetFunction", e);
   }
-  e = hipMalloc(reinterpret_cast<void**>(&g->d_res), sizeof(Res));
+  e = hipEventCreateWithFlags(&g->packed, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&g->d_res), sizeof(Res));
   if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&g->h_res), sizeof(Res), hipHostMallocDefault);
   if (e != hipSuccess) return hip_fail("rtn_pcap_next_batch_gpu: result block", e);
   g->device = device;
@@ -471,7 +474,7 @@ int32_t reserve(State* g, uint64_t bytes, uint32_t cap) {
 // of the mapping is read from the page cache here)
 void copy_in(const uint8_t* src, uint8_t* dst, size_t len) {
   const unsigned hw = std::thread::hardware_concurrency();
-  const size_t parts = std::min<size_t>(std::max(1u, std::min(hw, 8u)), std::max<size_t>(1, len >> 21));
+  const size_t parts = std::min<size_t>(std::max(1u, std::min(hw, 12u)), std::max<size_t>(1, len >> 20));
   if (parts <= 1) {
     memcpy(dst, src, len);
     return;
@@ -519,6 +522,8 @@ int32_t rtn_pcap_next_batch_gpu(rtn_pcap_t* p, int device, const rtn_stage_slab_
   hipError_t e = hipSetDevice(device);
   if (e != hipSuccess) return hip_fail("hipSetDevice", e);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  e = hipStreamWaitEvent(s, g->packed, 0);  // the previous batch's packing, on whatever stream
+  if (e != hipSuccess) return hip_fail("hipStreamWaitEvent", e);
   // pcapng: the section's byte order, from the first section header when walking from the start
   if (p->fmt == Fmt::Pcapng && p->off == p->first && p->size >= 12) {
     uint32_t bom;
@@ -622,6 +627,7 @@ int32_t rtn_pcap_next_batch_gpu(rtn_pcap_t* p, int device, const rtn_stage_slab_
       void* pp[] = {&pa};
       const uint32_t chunks = (tgt + RTN_CHUNK_FRAMES - 1) / RTN_CHUNK_FRAMES;
       e = hipModuleLaunchKernel(g->pack, (chunks + 3) / 4, 1, 1, 256, 1, 1, 0, s, pp, nullptr);
+      if (e == hipSuccess) e = hipEventRecord(g->packed, s);
       if (e != hipSuccess) return hip_fail("rtn_cap_pack", e);
       *n = tgt;
     }
