@@ -598,7 +598,9 @@ int32_t rtn_pcap_next_batch_gpu(rtn_pcap_t* p, int device, const rtn_stage_slab_
     const Res r = *g->h_res;
     const uint32_t recs = r.red[2], kept = r.red[3], tgt = r.tgt[0], bad = r.tgt[1];
     const uint64_t ex = r.cut[2];
-    if ((ex & kStop) && (ex & kErr) && tgt == kept)
+    // a pcapng section in the other byte order: the frames before it, then the error at it
+    const bool order = (ex & kStop) && (ex & kErr) && tgt == kept;
+    if (order && tgt == 0)
       return rtn::set_error(RTN_EINVAL, "pcapng sections in different byte orders: use rtn_pcap_next_batch_split");
     if (tgt < kept) {  // cut by cap or by a frame longer than 65535 bytes
       p->off += r.cut[0];
@@ -607,8 +609,8 @@ int32_t rtn_pcap_next_batch_gpu(rtn_pcap_t* p, int device, const rtn_stage_slab_
     } else {
       p->st.frames += recs;
       p->st.skipped_mtu += recs - kept;
-      if (ex & kDead) {  // the chain reached a record no candidate matched: the next batch starts there
-        p->off += ex & kOffMask;
+      if ((ex & kDead) || order) {  // the chain reached a record no candidate matched (or the
+        p->off += ex & kOffMask;      // section header): the next batch starts there
       } else if (!(ex & kStop)) {
         p->off += bytes;
       } else if ((ex & kEof) || at_eof) {

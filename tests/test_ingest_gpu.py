@@ -227,3 +227,26 @@ def test_host_and_gpu_batches_share_the_position(tmp_path, gpu):
         if k == 0:
             break
     assert [(f[:min(len(f), 64)], len(f)) for f in want] == got
+
+
+@pytest.mark.gpu
+def test_pcapng_sections_in_other_byte_order(tmp_path, gpu):
+    """The GPU walk takes one byte order per capture: the frames before a section header of the
+    other order, then RTN_EINVAL there (the host reader, which switches, takes the rest)."""
+    a, b = tmp_path / "a.pcapng", tmp_path / "b.pcapng"
+    _write_pcapng(a, _frames(60), big=False)
+    _write_pcapng(b, _frames(40), big=True)
+    p = tmp_path / "ab.pcapng"
+    p.write_bytes(a.read_bytes() + b.read_bytes())
+    first = opcap.offline_frames(a)
+    r = pc.PcapReader(p)
+    bufs = _Batches(1000)
+    got = []
+    with pytest.raises(pc.RetinaError) as e:
+        while True:
+            n = r.next_batch_gpu(bufs.head, bufs.ext, bufs.chunk, bufs.dl)
+            assert n > 0
+            got += bufs.frames(n)
+    assert e.value.code == -22
+    assert [(x[0], x[1]) for x in got] == [(f[:min(len(f), 128 if g[2] else 64)], len(f)) for f, g in zip(first, got)]
+    assert len(got) == len(first)
