@@ -109,14 +109,15 @@ __device__ __forceinline__ rtn_cap_rec rtn_cap_read(const rtn_cap_args& a, rtn_u
   // pcapng: type, block total length, body, block total length
   if (off + 12u > a.bytes) { r.kind = past; return r; }
   const rtn_u32 type = rtn_cap_ld32(a.win, off, sw);
-  const rtn_u32 blen = rtn_cap_ld32(a.win, off + 4u, sw);
-  if (blen < 12u) { r.kind = 2u; return r; }
-  r.len = blen;
-  if (off + blen > a.bytes) { r.kind = past; return r; }
+  // a section header in the other byte order (its length reads wrong in this one)
   if (type == 0x0A0D0D0Au && rtn_cap_ld32(a.win, off + 8u, false) != (sw ? 0x4D3C2B1Au : 0x1A2B3C4Du)) {
     r.kind = 3u;
     return r;
   }
+  const rtn_u32 blen = rtn_cap_ld32(a.win, off + 4u, sw);
+  if (blen < 12u) { r.kind = 2u; return r; }
+  r.len = blen;
+  if (off + blen > a.bytes) { r.kind = past; return r; }
   if (type == 6u && blen >= 32u) {  // enhanced packet block
     r.caplen = rtn_cap_ld32(a.win, off + 20u, sw);
     r.origlen = rtn_cap_ld32(a.win, off + 24u, sw);
