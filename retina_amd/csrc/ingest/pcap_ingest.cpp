@@ -12,6 +12,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -290,8 +291,9 @@ void rtn_pcap_close(rtn_pcap_t* p) {
 
 // ---------------------------------------------------------------------------------------------
 // rtn_pcap_next_batch_gpu: the capture walk on the GPU (csrc/kernels/capwalk_kernel.hip). A window
-// of the file, starting at a record, is copied to HBM as it is (worker threads copy the mapped
-// file into pinned memory, then one host -> HBM copy); the kernels find the window's record
+// of the file, starting at a record, is copied to HBM as it is (the window's pages of the file
+// mapping are registered with HIP and the copy engine reads them; if registration fails, worker
+// threads copy them into pinned memory first); the kernels find the window's record
 // chain, apply the offline runtime's rules and pack the kept frames into the gather layout of
 // rtn_stage_gather; the window stays resident, so a batch cut short by `cap` continues from it.
 namespace rtn_gpu_walk {
@@ -346,6 +348,11 @@ struct State {
   uint64_t d_win_cap = 0;
   uint8_t* h_stage = nullptr;  // pinned
   uint64_t h_cap = 0;
+  // the window's pages of the file mapping, registered with HIP so the copy engine reads them
+  // directly (no host copy); -1: registration failed once (or RTN_GPU_WALK_STAGED is set), so
+  // windows go through h_stage
+  void* reg = nullptr;
+  int reg_mode = 0;
   uint8_t* d_seg = nullptr;  // per-segment / per-node arrays for seg_cap segments
   uint32_t seg_cap = 0;
   Res* d_res = nullptr;
@@ -358,11 +365,16 @@ struct State {
   bool win_valid = false;
   uint64_t last_batch = 0;  // file bytes the last batch consumed
   hipEvent_t packed = nullptr;  // after the last batch's packing (it reads the window and frame list)
+  hipEvent_t copied = nullptr;  // after the last window copy (it reads reg / h_stage)
 };
 
 void destroy(State* g) {
   if (!g) return;
   if (g->device >= 0) (void)hipSetDevice(g->device);
+  if (g->reg) {
+    (void)hipEventSynchronize(g->copied);  // the last window copy may still read the pages
+    (void)hipHostUnregister(g->reg);
+  }
   if (g->d_win) (void)hipFree(g->d_win);
   if (g->h_stage) (void)hipHostFree(g->h_stage);
   if (g->d_seg) (void)hipFree(g->d_seg);
@@ -371,6 +383,7 @@ void destroy(State* g) {
   if (g->d_ptrs) (void)hipFree(g->d_ptrs);
   if (g->d_dl) (void)hipFree(g->d_dl);
   if (g->packed) (void)hipEventDestroy(g->packed);
+  if (g->copied) (void)hipEventDestroy(g->copied);
   if (g->module) (void)hipModuleUnload(g->module);
   delete g;
 }
@@ -395,9 +408,13 @@ int32_t init(State* g, int device) {
     if (e != hipSuccess) return hip_fail("hipModuleGetFunction", e);
   }
   e = hipEventCreateWithFlags(&g->packed, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&g->copied, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventRecord(g->copied, nullptr);
   if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&g->d_res), sizeof(Res));
   if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&g->h_res), sizeof(Res), hipHostMallocDefault);
   if (e != hipSuccess) return hip_fail("rtn_pcap_next_batch_gpu: result block", e);
+  const char* v = getenv("RTN_GPU_WALK_STAGED");  // diagnostics: the staged copy, for comparison
+  g->reg_mode = v && *v && *v != '0' ? -1 : 1;
   g->device = device;
   return RTN_OK;
 }
@@ -442,7 +459,7 @@ int32_t reserve(State* g, uint64_t bytes, uint32_t cap) {
     g->d_win_cap = bytes + kPad;
     g->win_valid = false;
   }
-  if (bytes > g->h_cap) {
+  if (bytes > g->h_cap && g->reg_mode < 0) {
     if (g->h_stage) (void)hipHostFree(g->h_stage);
     g->h_stage = nullptr;
     e = hipHostMalloc(reinterpret_cast<void**>(&g->h_stage), bytes, hipHostMallocDefault);
@@ -546,16 +563,36 @@ int32_t rtn_pcap_next_batch_gpu(rtn_pcap_t* p, int device, const rtn_stage_slab_
     const size_t off0 = p->off;
     if (fresh) {
       prefault(p, p->off, want);
-      e = hipStreamSynchronize(s);  // the staging buffer's previous copy has left
-      if (e != hipSuccess) return hip_fail("hipStreamSynchronize", e);
+      e = hipEventSynchronize(g->copied);  // the previous window's copy has left its source
+      if (e != hipSuccess) return hip_fail("hipEventSynchronize", e);
+      if (g->reg) {  // the previous window's pages
+        (void)hipHostUnregister(g->reg);
+        g->reg = nullptr;
+      }
+      e = hipSuccess;
+      if (g->reg_mode > 0) {  // page-aligned cover of [off, off + want) inside the mapping
+        const uintptr_t b0 = reinterpret_cast<uintptr_t>(p->base + p->off) & ~uintptr_t(4095);
+        const uintptr_t b1 = (reinterpret_cast<uintptr_t>(p->base + p->off + want) + 4095) & ~uintptr_t(4095);
+        e = hipHostRegister(reinterpret_cast<void*>(b0), b1 - b0, hipHostRegisterReadOnly);
+        if (e == hipSuccess) {
+          g->reg = reinterpret_cast<void*>(b0);
+          e = hipMemcpyAsync(g->d_win, p->base + p->off, want, hipMemcpyHostToDevice, s);
+        } else {
+          (void)hipGetLastError();
+          g->reg_mode = -1;
+          e = hipSuccess;
+          rc = reserve(g, std::min<uint64_t>(g->window, p->size - p->first), slab->cap);  // the staging buffer
+          if (rc) return rc;
+        }
+      }
       // 16-MiB pieces: the host copies piece k + 1 while the copy engine moves piece k
       constexpr uint64_t kPiece = 16ull << 20;
-      e = hipSuccess;
-      for (uint64_t a0 = 0; a0 < want && e == hipSuccess; a0 += kPiece) {
+      for (uint64_t a0 = 0; g->reg_mode < 0 && a0 < want && e == hipSuccess; a0 += kPiece) {
         const uint64_t len = std::min(kPiece, want - a0);
         copy_in(p->base + p->off + a0, g->h_stage + a0, len);
         e = hipMemcpyAsync(g->d_win + a0, g->h_stage + a0, len, hipMemcpyHostToDevice, s);
       }
+      if (e == hipSuccess) e = hipEventRecord(g->copied, s);
       if (e == hipSuccess) e = hipMemsetAsync(g->d_win + want, 0, kPad, s);
       if (e != hipSuccess) return hip_fail("window copy", e);
       g->win_off = p->off;

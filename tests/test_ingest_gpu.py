@@ -250,3 +250,17 @@ def test_pcapng_sections_in_other_byte_order(tmp_path, gpu):
     assert e.value.code == -22
     assert [(x[0], x[1]) for x in got] == [(f[:min(len(f), 128 if g[2] else 64)], len(f)) for f, g in zip(first, got)]
     assert len(got) == len(first)
+
+
+@pytest.mark.gpu
+def test_staged_window_copy(tmp_path, gpu, monkeypatch):
+    """The fallback window copy (worker threads into pinned memory, taken when the file's pages
+    cannot be registered; forced here by RTN_GPU_WALK_STAGED): the same frames."""
+    monkeypatch.setenv("RTN_GPU_WALK_STAGED", "1")
+    slab, dlen, stride, _ = corpus("cfg3", 30000)
+    p = tmp_path / "c.pcap"
+    _write_pcap(p, _slab_frames(slab, dlen, stride))
+    _check(p, 9702, 4096, 1 << 20)
+    p2 = tmp_path / "a.pcapng"
+    _write_pcapng(p2, _frames(600), big=True)
+    _check(p2, 9702, 37, 1 << 16)

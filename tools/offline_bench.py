@@ -7,6 +7,8 @@ summary lines.
 """
 from __future__ import annotations
 
+import json
+import os
 import struct
 import subprocess
 import sys
@@ -58,14 +60,19 @@ def main() -> None:
         spec = Path(d) / "spec.toml"
         spec.write_text(bench.spec_for(cfg))
         exe = ROOT / "retina_amd" / "_lib" / "rtn_offline"
-        for layout in ("gpu", "compact", "mono"):
+        # gpu: the window's file pages registered and copied by the copy engine; gpu-staged: the
+        # fallback, worker threads copying them into pinned memory first (RTN_GPU_WALK_STAGED)
+        for name, layout in (("gpu", "gpu"), ("gpu-staged", "gpu"), ("compact", "compact"), ("mono", "mono")):
+            env = dict(os.environ, RTN_GPU_WALK_STAGED="1" if name == "gpu-staged" else "0")
             for _ in range(2):  # the second run has the capture in the page cache
                 r = subprocess.run([str(exe), str(spec), str(cap), "--layout", layout, *extra],
-                                   capture_output=True, text=True, timeout=300)
+                                   capture_output=True, text=True, timeout=300, env=env)
                 if r.returncode:
                     sys.stderr.write(r.stderr)
                     raise SystemExit(r.returncode)
-            print(r.stdout.strip().splitlines()[-1], flush=True)
+            line = json.loads(r.stdout.strip().splitlines()[-1])
+            line["walk"] = name
+            print(json.dumps(line), flush=True)
 
 
 if __name__ == "__main__":
