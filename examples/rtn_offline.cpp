@@ -144,14 +144,14 @@ void walk(const HostSet& h, bool with_ct, Totals& t, FILE* dump) {
 int main(int argc, char** argv) {
   if (argc < 3) {
     fprintf(stderr, "usage: rtn_offline <spec.toml> <capture> [--batch N] [--mtu M] [--device D] [--no-ct] "
-                    "[--ct-log2 L] [--max-conn C] [--dump FILE] [--layout compact|mono|gpu] [--window BYTES]\n");
+                    "[--ct-log2 L] [--max-conn C] [--dump FILE] [--layout compact|mono|gpu] [--window BYTES] [--one-stream]\n");
     return 2;
   }
   uint32_t batch = 1u << 20, mtu = 9702, ct_log2 = 24, max_conn = 10000000;  // configs/offline.toml
   int device = 0;
   bool with_ct = true;
   const char* dump_path = nullptr;
-  bool compact = true, gpu_walk = false;  // gpu: the capture walk on the GPU (rtn_pcap_next_batch_gpu)
+  bool compact = true, gpu_walk = false, one_stream = false;  // gpu: the capture walk on the GPU (rtn_pcap_next_batch_gpu)
   uint64_t window = 0;
   for (int a = 3; a < argc; ++a) {
     std::string s = argv[a];
@@ -170,6 +170,7 @@ int main(int argc, char** argv) {
       gpu_walk = l == "gpu";
     }
     else if (s == "--window") window = strtoull(next(), nullptr, 10);
+    else if (s == "--one-stream") one_stream = true;  // gpu: the walk on the stages' stream
     else die(("unknown option " + s).c_str(), -22);
   }
   batch = (batch + RTN_CHUNK_FRAMES - 1) / RTN_CHUNK_FRAMES * RTN_CHUNK_FRAMES;
@@ -216,6 +217,22 @@ int main(int argc, char** argv) {
     if (info.conn_words) out.conn_dlv = dev_alloc<uint64_t>(rtn_out_conn_dlv_bytes(batch, info.conn_words));
     d_ct = dev_alloc<rtn_ct_entry_t>(rtn_out_ct_bytes(batch));
   }
+  // --layout gpu: the batch is packed on the device, so the device slab is the double buffer (the
+  // walk of batch k + 1 runs on its own stream while batch k runs through the stages)
+  uint8_t* g_slab[2] = {d_slab, nullptr};
+  uint8_t* g_ext[2] = {d_ext, nullptr};
+  uint32_t* g_chunk[2] = {d_chunk, nullptr};
+  uint16_t* g_dlen[2] = {d_dlen, nullptr};
+  hipStream_t wstream = nullptr;
+  hipEvent_t walked = nullptr;
+  if (gpu_walk) {
+    g_slab[1] = dev_alloc<uint8_t>(batch * stride);
+    g_ext[1] = dev_alloc<uint8_t>((size_t)batch * 64u);
+    g_chunk[1] = dev_alloc<uint32_t>(nchunks * 4u);
+    g_dlen[1] = dev_alloc<uint16_t>(batch * 2u);
+    HIP_CHECK(hipStreamCreateWithFlags(&wstream, hipStreamNonBlocking));
+    HIP_CHECK(hipEventCreateWithFlags(&walked, hipEventDisableTiming));
+  }
   HostSet hs[2];
   for (auto& h : hs) {
     h.slab = host_alloc<uint8_t>(batch * stride);
@@ -253,8 +270,17 @@ int main(int argc, char** argv) {
     uint32_t n = 0;
     const auto tp = now();
     if (gpu_walk) {  // the file's bytes to HBM, records found and frames packed by the GPU
+      // (into the device set batch it - 2 used: its results were waited for above)
+      d_slab = g_slab[it & 1u];
+      d_ext = g_ext[it & 1u];
+      d_chunk = g_chunk[it & 1u];
+      d_dlen = g_dlen[it & 1u];
       rtn_stage_slab_t sl = {d_slab, d_ext, d_chunk, d_dlen, batch, batch};
-      RTN_CHECK(rtn_pcap_next_batch_gpu(cap, device, &sl, &n, stream));
+      RTN_CHECK(rtn_pcap_next_batch_gpu(cap, device, &sl, &n, one_stream ? stream : wstream));
+      if (!one_stream) {
+        HIP_CHECK(hipEventRecord(walked, wstream));
+        HIP_CHECK(hipStreamWaitEvent(stream, walked, 0));
+      }
     } else if (compact) {
       RTN_CHECK(rtn_pcap_next_batch_split(cap, h.slab, h.ext, batch, h.ext_chunk, h.dlen, batch, &n, &h.rows));
     } else {

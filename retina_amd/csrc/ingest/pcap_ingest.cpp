@@ -344,8 +344,13 @@ struct State {
   hipModule_t module = nullptr;
   hipFunction_t cand = nullptr, nodes = nullptr, jump = nullptr, lift = nullptr, scan = nullptr, emit = nullptr,
                 pack = nullptr;
-  uint8_t* d_win = nullptr;  // window + kPad
-  uint64_t d_win_cap = 0;
+  // two device buffers of 2 * half + kPad bytes: a window sits at [half, 2 * half) of one, the
+  // next window's bytes are prefetched into the other's second half while the batches of the
+  // current one run, and the current window's unread tail is moved in front of them on the switch
+  uint8_t* d_buf[2] = {nullptr, nullptr};
+  uint64_t half = 0;
+  int cur = 0;
+  uint8_t* win_ptr = nullptr;  // the resident window's first byte
   uint8_t* h_stage = nullptr;  // pinned
   uint64_t h_cap = 0;
   // the window's pages of the file mapping, registered with HIP so the copy engine reads them
@@ -353,6 +358,13 @@ struct State {
   // windows go through h_stage
   void* reg = nullptr;
   int reg_mode = 0;
+  // the prefetch of file bytes [pf_off, pf_off + pf_len) into d_buf[1 - cur] + half, on cs;
+  // pf_reg: its registered pages (the first partial page is read through reg)
+  hipStream_t cs = nullptr;
+  hipEvent_t pf_done = nullptr, s_ready = nullptr;
+  bool pf_valid = false;
+  uint64_t pf_off = 0, pf_len = 0;
+  void* pf_reg = nullptr;
   uint8_t* d_seg = nullptr;  // per-segment / per-node arrays for seg_cap segments
   uint32_t seg_cap = 0;
   Res* d_res = nullptr;
@@ -360,22 +372,37 @@ struct State {
   uint64_t* d_ptrs = nullptr;
   uint16_t* d_dl = nullptr;
   uint32_t list_cap = 0;
-  // the resident window: file bytes [win_off, win_off + win_len) at d_win
+  // the resident window: file bytes [win_off, win_off + win_len) at win_ptr
   size_t win_off = 0, win_len = 0;
   bool win_valid = false;
   uint64_t last_batch = 0;  // file bytes the last batch consumed
+  double bpf = 0;           // ... per frame it packed
   hipEvent_t packed = nullptr;  // after the last batch's packing (it reads the window and frame list)
   hipEvent_t copied = nullptr;  // after the last window copy (it reads reg / h_stage)
 };
 
+// Waits for an outstanding prefetch and forgets it.
+void drop_prefetch(State* g) {
+  if (!g->pf_valid) return;
+  (void)hipEventSynchronize(g->pf_done);
+  if (g->pf_reg) (void)hipHostUnregister(g->pf_reg);
+  g->pf_reg = nullptr;
+  g->pf_valid = false;
+}
+
 void destroy(State* g) {
   if (!g) return;
   if (g->device >= 0) (void)hipSetDevice(g->device);
+  drop_prefetch(g);
   if (g->reg) {
     (void)hipEventSynchronize(g->copied);  // the last window copy may still read the pages
     (void)hipHostUnregister(g->reg);
   }
-  if (g->d_win) (void)hipFree(g->d_win);
+  for (uint8_t* b : g->d_buf)
+    if (b) (void)hipFree(b);
+  if (g->cs) (void)hipStreamDestroy(g->cs);
+  if (g->pf_done) (void)hipEventDestroy(g->pf_done);
+  if (g->s_ready) (void)hipEventDestroy(g->s_ready);
   if (g->h_stage) (void)hipHostFree(g->h_stage);
   if (g->d_seg) (void)hipFree(g->d_seg);
   if (g->d_res) (void)hipFree(g->d_res);
@@ -410,6 +437,9 @@ int32_t init(State* g, int device) {
   e = hipEventCreateWithFlags(&g->packed, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&g->copied, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventRecord(g->copied, nullptr);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&g->pf_done, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&g->s_ready, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&g->cs, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&g->d_res), sizeof(Res));
   if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&g->h_res), sizeof(Res), hipHostMallocDefault);
   if (e != hipSuccess) return hip_fail("rtn_pcap_next_batch_gpu: result block", e);
@@ -451,13 +481,20 @@ void carve(uint8_t* q, uint32_t nseg_cap, CapArgs& a) {
 // Buffers for a window of `bytes` and a batch of `cap` frames (grown, never shrunk).
 int32_t reserve(State* g, uint64_t bytes, uint32_t cap) {
   hipError_t e = hipSuccess;
-  if (bytes + kPad > g->d_win_cap) {
-    if (g->d_win) (void)hipFree(g->d_win);
-    g->d_win = nullptr;
-    e = hipMalloc(reinterpret_cast<void**>(&g->d_win), bytes + kPad);
-    if (e != hipSuccess) return hip_fail("hipMalloc (window)", e);
-    g->d_win_cap = bytes + kPad;
+  if (bytes > g->half) {
+    drop_prefetch(g);
+    (void)hipDeviceSynchronize();  // work still reading the old window
+    for (uint8_t*& b : g->d_buf) {
+      if (b) (void)hipFree(b);
+      b = nullptr;
+    }
+    g->half = 0;
     g->win_valid = false;
+    for (uint8_t*& b : g->d_buf) {
+      e = hipMalloc(reinterpret_cast<void**>(&b), 2 * bytes + kPad);
+      if (e != hipSuccess) return hip_fail("hipMalloc (window)", e);
+    }
+    g->half = bytes;
   }
   if (bytes > g->h_cap && g->reg_mode < 0) {
     if (g->h_stage) (void)hipHostFree(g->h_stage);
@@ -466,7 +503,7 @@ int32_t reserve(State* g, uint64_t bytes, uint32_t cap) {
     if (e != hipSuccess) return hip_fail("hipHostMalloc (window)", e);
     g->h_cap = bytes;
   }
-  const uint32_t nseg = (uint32_t)((bytes + kSeg - 1) / kSeg);
+  const uint32_t nseg = (uint32_t)((2 * bytes + kSeg - 1) / kSeg);  // a window plus a moved tail
   if (nseg > g->seg_cap) {
     if (g->d_seg) (void)hipFree(g->d_seg);
     g->d_seg = nullptr;
@@ -484,6 +521,37 @@ int32_t reserve(State* g, uint64_t bytes, uint32_t cap) {
     if (e != hipSuccess) return hip_fail("hipMalloc (frame list)", e);
     g->list_cap = cap;
   }
+  return RTN_OK;
+}
+
+// Starts copying the file bytes that follow the resident window into d_buf[1 - cur] + half, on
+// cs after the work enqueued on s so far (it may still read that buffer). Registered mode only.
+int32_t prefetch(rtn_pcap* p, State* g, hipStream_t s) {
+  const uint64_t off = g->win_off + g->win_len;
+  if (g->reg_mode <= 0 || off >= p->size) return RTN_OK;
+  const uint64_t len = std::min<uint64_t>({g->window, p->size - off, g->half});
+  uint8_t* dst = g->d_buf[1 - g->cur] + g->half;
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p->base + off);
+  const uintptr_t a1 = (a + 4095) & ~uintptr_t(4095), b1 = (a + len + 4095) & ~uintptr_t(4095);
+  const uint64_t head = std::min<uint64_t>(len, a1 - a);  // inside the window's last registered page
+  hipError_t e = hipEventRecord(g->s_ready, s);
+  if (e == hipSuccess) e = hipStreamWaitEvent(g->cs, g->s_ready, 0);
+  if (e == hipSuccess && len > head) {
+    if (hipHostRegister(reinterpret_cast<void*>(a1), b1 - a1, hipHostRegisterReadOnly) != hipSuccess) {
+      (void)hipGetLastError();
+      return RTN_OK;  // no prefetch: the next window is copied when it is needed
+    }
+    g->pf_reg = reinterpret_cast<void*>(a1);
+  }
+  if (e == hipSuccess && head) e = hipMemcpyAsync(dst, p->base + off, head, hipMemcpyHostToDevice, g->cs);
+  if (e == hipSuccess && len > head)
+    e = hipMemcpyAsync(dst + head, p->base + off + head, len - head, hipMemcpyHostToDevice, g->cs);
+  if (e == hipSuccess) e = hipMemsetAsync(dst + len, 0, kPad, g->cs);
+  if (e == hipSuccess) e = hipEventRecord(g->pf_done, g->cs);
+  if (e != hipSuccess) return hip_fail("window prefetch", e);
+  g->pf_valid = true;
+  g->pf_off = off;
+  g->pf_len = len;
   return RTN_OK;
 }
 
@@ -514,7 +582,7 @@ int32_t rtn_pcap_gpu_window(rtn_pcap_t* p, uint64_t bytes) {
   if (bytes < (1u << 16) || bytes > (1ull << 40)) return rtn::set_error(RTN_EINVAL, "window of 64 KiB .. 1 TiB");
   if (!p->gpu) p->gpu = new rtn_gpu_walk::State();
   p->gpu->window = bytes;
-  p->gpu->win_valid = false;
+  p->gpu->win_valid = false;  // (an outstanding prefetch is dropped at the next batch)
   return RTN_OK;
 }
 
@@ -561,6 +629,35 @@ int32_t rtn_pcap_next_batch_gpu(rtn_pcap_t* p, int device, const rtn_stage_slab_
       fresh = left < std::max<uint64_t>(g->last_batch, 1u << 20) && g->win_off + g->win_len < p->size;
     }
     const size_t off0 = p->off;
+    if (fresh && g->pf_valid) {
+      // the prefetched bytes follow the window: move its unread tail in front of them
+      const bool follows = g->win_valid && g->pf_off == g->win_off + g->win_len && p->off >= g->win_off &&
+                           p->off <= g->pf_off && g->pf_off - p->off <= g->half;
+      if (follows) {
+        const uint64_t tail = g->pf_off - p->off;
+        uint8_t* nb = g->d_buf[1 - g->cur] + g->half - tail;
+        e = hipEventSynchronize(g->pf_done);  // (the prefetch's first page is read through reg)
+        if (e == hipSuccess) e = hipStreamWaitEvent(s, g->pf_done, 0);
+        if (e == hipSuccess && tail)
+          e = hipMemcpyAsync(nb, g->win_ptr + (p->off - g->win_off), tail, hipMemcpyDeviceToDevice, s);
+        if (e != hipSuccess) return hip_fail("window switch", e);
+        if (g->pf_reg) {
+          if (g->reg) (void)hipHostUnregister(g->reg);
+          g->reg = g->pf_reg;
+          g->pf_reg = nullptr;
+        }
+        g->pf_valid = false;
+        g->cur = 1 - g->cur;
+        g->win_ptr = nb;
+        g->win_off = p->off;
+        g->win_len = tail + g->pf_len;
+        fresh = false;
+        int32_t prc = prefetch(p, g, s);
+        if (prc) return prc;
+      } else {
+        drop_prefetch(g);
+      }
+    }
     if (fresh) {
       prefault(p, p->off, want);
       e = hipEventSynchronize(g->copied);  // the previous window's copy has left its source
@@ -569,6 +666,7 @@ int32_t rtn_pcap_next_batch_gpu(rtn_pcap_t* p, int device, const rtn_stage_slab_
         (void)hipHostUnregister(g->reg);
         g->reg = nullptr;
       }
+      g->win_ptr = g->d_buf[g->cur] + g->half;
       e = hipSuccess;
       if (g->reg_mode > 0) {  // page-aligned cover of [off, off + want) inside the mapping
         const uintptr_t b0 = reinterpret_cast<uintptr_t>(p->base + p->off) & ~uintptr_t(4095);
@@ -576,7 +674,7 @@ int32_t rtn_pcap_next_batch_gpu(rtn_pcap_t* p, int device, const rtn_stage_slab_
         e = hipHostRegister(reinterpret_cast<void*>(b0), b1 - b0, hipHostRegisterReadOnly);
         if (e == hipSuccess) {
           g->reg = reinterpret_cast<void*>(b0);
-          e = hipMemcpyAsync(g->d_win, p->base + p->off, want, hipMemcpyHostToDevice, s);
+          e = hipMemcpyAsync(g->win_ptr, p->base + p->off, want, hipMemcpyHostToDevice, s);
         } else {
           (void)hipGetLastError();
           g->reg_mode = -1;
@@ -590,49 +688,66 @@ int32_t rtn_pcap_next_batch_gpu(rtn_pcap_t* p, int device, const rtn_stage_slab_
       for (uint64_t a0 = 0; g->reg_mode < 0 && a0 < want && e == hipSuccess; a0 += kPiece) {
         const uint64_t len = std::min(kPiece, want - a0);
         copy_in(p->base + p->off + a0, g->h_stage + a0, len);
-        e = hipMemcpyAsync(g->d_win + a0, g->h_stage + a0, len, hipMemcpyHostToDevice, s);
+        e = hipMemcpyAsync(g->win_ptr + a0, g->h_stage + a0, len, hipMemcpyHostToDevice, s);
       }
       if (e == hipSuccess) e = hipEventRecord(g->copied, s);
-      if (e == hipSuccess) e = hipMemsetAsync(g->d_win + want, 0, kPad, s);
+      if (e == hipSuccess) e = hipMemsetAsync(g->win_ptr + want, 0, kPad, s);
       if (e != hipSuccess) return hip_fail("window copy", e);
       g->win_off = p->off;
       g->win_len = want;
       g->win_valid = true;
+      rc = prefetch(p, g, s);
+      if (rc) return rc;
     }
     const uint64_t rel = p->off - g->win_off, bytes = g->win_len - rel;
     const bool at_eof = g->win_off + g->win_len == p->size;
-    CapArgs a{};
-    a.win = g->d_win + rel;
-    a.bytes = bytes;
-    a.nseg = (uint32_t)((bytes + kSeg - 1) / kSeg);
-    a.fmt = p->fmt == Fmt::Pcapng ? 1u : 0u;
-    a.swap = swap ? 1u : 0u;
-    a.mtu = p->mtu;
-    a.at_eof = at_eof ? 1u : 0u;
-    carve(g->d_seg, g->seg_cap, a);
-    a.levels = levels(a.nseg);
-    a.red = g->d_res->red;
-    a.tgt = g->d_res->tgt;
-    a.cut = g->d_res->cut;
-    a.cap = slab->cap;
-    a.ptrs = g->d_ptrs;
-    a.dlen = g->d_dl;
-    void* params[] = {&a};
-    e = hipMemsetAsync(g->d_res, 0, sizeof(Res), s);
-    const uint32_t nb4 = (a.nseg + 3) / 4, nb256 = (a.nseg + 255) / 256, nbn = (a.nseg * kCand + 255) / 256;
-    if (e == hipSuccess) e = hipModuleLaunchKernel(g->cand, nb4, 1, 1, 256, 1, 1, 0, s, params, nullptr);
-    if (e == hipSuccess) e = hipModuleLaunchKernel(g->nodes, nbn, 1, 1, 256, 1, 1, 0, s, params, nullptr);
-    for (uint32_t k = 1; k <= a.levels && e == hipSuccess; ++k) {
-      a.k = k;  // (the launch copies the arguments)
-      e = hipModuleLaunchKernel(g->jump, nbn, 1, 1, 256, 1, 1, 0, s, params, nullptr);
+    // The walk covers the bytes the batch is expected to need (the last batch's file bytes per
+    // packed frame, with a margin) when that is less than the window; its answer is taken only
+    // if it holds more than `cap` kept frames (so it equals the whole window's), else the whole
+    // window is walked.
+    uint64_t lim = bytes;
+    if (g->bpf > 0) {
+      const double est = g->bpf * slab->cap * 1.25 + (256u << 10);
+      if (est < (double)bytes) lim = ((uint64_t)est + kSeg - 1) & ~(kSeg - 1);
     }
-    if (e == hipSuccess) e = hipModuleLaunchKernel(g->lift, nb256, 1, 1, 256, 1, 1, 0, s, params, nullptr);
-    if (e == hipSuccess) e = hipModuleLaunchKernel(g->scan, 1, 1, 1, 1024, 1, 1, 0, s, params, nullptr);
-    if (e == hipSuccess) e = hipModuleLaunchKernel(g->emit, nb256, 1, 1, 256, 1, 1, 0, s, params, nullptr);
-    if (e == hipSuccess) e = hipMemcpyAsync(g->h_res, g->d_res, sizeof(Res), hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess) e = hipStreamSynchronize(s);
-    if (e != hipSuccess) return hip_fail("rtn_pcap_next_batch_gpu", e);
-    const Res r = *g->h_res;
+    CapArgs a{};
+    Res r{};
+    for (;;) {
+      a = CapArgs{};
+      a.win = g->win_ptr + rel;
+      a.bytes = lim;
+      a.nseg = (uint32_t)((lim + kSeg - 1) / kSeg);
+      a.fmt = p->fmt == Fmt::Pcapng ? 1u : 0u;
+      a.swap = swap ? 1u : 0u;
+      a.mtu = p->mtu;
+      a.at_eof = at_eof && lim == bytes ? 1u : 0u;
+      carve(g->d_seg, g->seg_cap, a);
+      a.levels = levels(a.nseg);
+      a.red = g->d_res->red;
+      a.tgt = g->d_res->tgt;
+      a.cut = g->d_res->cut;
+      a.cap = slab->cap;
+      a.ptrs = g->d_ptrs;
+      a.dlen = g->d_dl;
+      void* params[] = {&a};
+      e = hipMemsetAsync(g->d_res, 0, sizeof(Res), s);
+      const uint32_t nb4 = (a.nseg + 3) / 4, nb256 = (a.nseg + 255) / 256, nbn = (a.nseg * kCand + 255) / 256;
+      if (e == hipSuccess) e = hipModuleLaunchKernel(g->cand, nb4, 1, 1, 256, 1, 1, 0, s, params, nullptr);
+      if (e == hipSuccess) e = hipModuleLaunchKernel(g->nodes, nbn, 1, 1, 256, 1, 1, 0, s, params, nullptr);
+      for (uint32_t k = 1; k <= a.levels && e == hipSuccess; ++k) {
+        a.k = k;  // (the launch copies the arguments)
+        e = hipModuleLaunchKernel(g->jump, nbn, 1, 1, 256, 1, 1, 0, s, params, nullptr);
+      }
+      if (e == hipSuccess) e = hipModuleLaunchKernel(g->lift, nb256, 1, 1, 256, 1, 1, 0, s, params, nullptr);
+      if (e == hipSuccess) e = hipModuleLaunchKernel(g->scan, 1, 1, 1, 1024, 1, 1, 0, s, params, nullptr);
+      if (e == hipSuccess) e = hipModuleLaunchKernel(g->emit, nb256, 1, 1, 256, 1, 1, 0, s, params, nullptr);
+      if (e == hipSuccess) e = hipMemcpyAsync(g->h_res, g->d_res, sizeof(Res), hipMemcpyDeviceToHost, s);
+      if (e == hipSuccess) e = hipStreamSynchronize(s);
+      if (e != hipSuccess) return hip_fail("rtn_pcap_next_batch_gpu", e);
+      r = *g->h_res;
+      if (lim == bytes || (r.tgt[0] == slab->cap && r.red[3] > slab->cap)) break;
+      lim = bytes;
+    }
     const uint32_t recs = r.red[2], kept = r.red[3], tgt = r.tgt[0], bad = r.tgt[1];
     const uint64_t ex = r.cut[2];
     // a pcapng section in the other byte order: the frames before it, then the error at it
@@ -661,6 +776,7 @@ int32_t rtn_pcap_next_batch_gpu(rtn_pcap_t* p, int device, const rtn_stage_slab_
     p->st.packed += tgt;
     p->st.bytes += r.cut[3];
     g->last_batch = p->off - off0;
+    if (tgt > 0) g->bpf = (double)g->last_batch / tgt;
     if (tgt > 0) {
       PackArgs pa{g->d_ptrs, g->d_dl, slab->head, slab->ext, slab->ext_chunk, slab->data_len, tgt};
       void* pp[] = {&pa};
