@@ -47,7 +47,7 @@ int32_t rtn_pcap_next_batch(rtn_pcap_t* p, uint8_t* slab, uint64_t stride, uint1
 int32_t rtn_pcap_next_batch_split(rtn_pcap_t* p, uint8_t* head, uint8_t* ext, uint32_t ext_cap, uint32_t* ext_chunk,
                                   uint16_t* data_len, uint32_t cap, uint32_t* n, uint32_t* rows);
 /* The same frames with the capture walk on the GPU (the host copies the file's bytes, the device
- * finds the records): a window of the capture (rtn_pcap_gpu_window, default 256 MiB) is copied to
+ * finds the records): a window of the capture (rtn_pcap_gpu_window, default 64 MiB) is copied to
  * HBM as it is (the copy engine reads the window's pages of the file mapping, registered with
  * HIP; the next window is prefetched on an internal stream while this one's batches run; device
  * memory: two buffers of twice the window), and gfx950 kernels find its record chain in parallel (speculated per 4-KiB

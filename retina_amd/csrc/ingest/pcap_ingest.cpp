@@ -340,7 +340,7 @@ struct Res {  // device result block, copied back once per window
 
 struct State {
   int device = -1;
-  uint64_t window = 256ull << 20;
+  uint64_t window = 64ull << 20;
   hipModule_t module = nullptr;
   hipFunction_t cand = nullptr, nodes = nullptr, jump = nullptr, lift = nullptr, scan = nullptr, emit = nullptr,
                 pack = nullptr;
