@@ -264,3 +264,37 @@ def test_staged_window_copy(tmp_path, gpu, monkeypatch):
     p2 = tmp_path / "a.pcapng"
     _write_pcapng(p2, _frames(600), big=True)
     _check(p2, 9702, 37, 1 << 16)
+
+
+@pytest.mark.gpu
+def test_frame_size_change_and_window_resize(tmp_path, gpu):
+    """Small frames then large ones (the walk bounded by the last batch's bytes per frame falls
+    short and the whole window is walked), and the window resized between batches while the next
+    one is being prefetched (smaller, then larger: the device buffers are reallocated)."""
+    import torch
+
+    small = [(bytes([i % 251]) * 60, 60) for i in range(3000)]
+    large = [(bytes([i % 241]) * 1400, 1400) for i in range(3000)]
+    p = tmp_path / "mix.pcap"
+    _write_pcap(p, small + large + small)
+    want = opcap.offline_frames(p)
+    r = pc.PcapReader(p)
+    r.gpu_window(1 << 20)
+    b = _Batches(500)
+    got = []
+    for turn in range(1000):
+        if turn == 3:
+            r.gpu_window(1 << 17)
+        elif turn == 9:
+            r.gpu_window(1 << 22)
+        n = r.next_batch_gpu(b.head, b.ext, b.chunk, b.dl)
+        torch.cuda.synchronize()
+        if n == 0:
+            break
+        got += b.frames(n)
+    assert len(got) == len(want)
+    for i, ((x, d, need), f) in enumerate(zip(got, want)):
+        assert d == len(f) and x == f[:min(len(f), 128 if need else 64)], i
+    host = pc.PcapReader(p)
+    host.read_all(stride=64, batch=4096)
+    assert r.stats() == host.stats()
