@@ -748,7 +748,7 @@ int32_t rtn_pcap_next_batch_gpu(rtn_pcap_t* p, int device, const rtn_stage_slab_
     uint64_t lim = bytes;
     if (g->bpf > 0) {
       const double est = g->bpf * slab->cap * 1.25 + (256u << 10);
-      if (est < (double)bytes) lim = ((uint64_t)est + kSeg - 1) & ~(kSeg - 1);
+      if (est < (double)bytes) lim = std::min<uint64_t>(bytes, ((uint64_t)est + kSeg - 1) & ~(kSeg - 1));
     }
     CapArgs a{};
     Res r{};
