@@ -56,7 +56,9 @@ int32_t rtn_pcap_next_batch_split(rtn_pcap_t* p, uint8_t* head, uint8_t* ext, ui
  * in device memory, in the gather layout of rtn_stage_gather (retina_stage.h: head slots, ext
  * rows compact within each chunk at rows [c * RTN_CHUNK_FRAMES, ...), ext_chunk[c] =
  * c * RTN_CHUNK_FRAMES; slab->ext_cap >= rtn_stage_gather_ext_rows(slab->cap)). The packing is
- * left running on `stream` (a hipStream_t; a later call on another stream waits for it); *n,
+ * left running on `stream` (a hipStream_t; a later call on another stream waits for it). A batch
+ * also ends at the end of a window, so it can hold fewer than slab->cap frames before the end of
+ * the file (size the window to about cap times the mean record to keep batches full); *n,
  * the stats and the file position are final on return. *n == 0 with RTN_OK means end of file. A kept frame longer
  * than 65535 bytes ends the batch before it with RTN_ERANGE (as rtn_pcap_next_batch); pcapng
  * sections in different byte orders are refused (RTN_EINVAL). Calls may be mixed with the host
