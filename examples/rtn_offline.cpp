@@ -23,6 +23,10 @@
 #include <hip/hip_runtime.h>
 
 #include <chrono>
+#include <condition_variable>
+#include <deque>
+#include <mutex>
+#include <thread>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -144,14 +148,14 @@ void walk(const HostSet& h, bool with_ct, Totals& t, FILE* dump) {
 int main(int argc, char** argv) {
   if (argc < 3) {
     fprintf(stderr, "usage: rtn_offline <spec.toml> <capture> [--batch N] [--mtu M] [--device D] [--no-ct] "
-                    "[--ct-log2 L] [--max-conn C] [--dump FILE] [--layout compact|mono|gpu] [--window BYTES] [--one-stream]\n");
+                    "[--ct-log2 L] [--max-conn C] [--dump FILE] [--layout compact|mono|gpu] [--window BYTES] [--one-stream] [--inline-results]\n");
     return 2;
   }
   uint32_t batch = 1u << 20, mtu = 9702, ct_log2 = 24, max_conn = 10000000;  // configs/offline.toml
   int device = 0;
   bool with_ct = true;
   const char* dump_path = nullptr;
-  bool compact = true, gpu_walk = false, one_stream = false;  // gpu: the capture walk on the GPU (rtn_pcap_next_batch_gpu)
+  bool compact = true, gpu_walk = false, one_stream = false, inline_results = false;  // gpu: the capture walk on the GPU (rtn_pcap_next_batch_gpu)
   uint64_t window = 0;
   for (int a = 3; a < argc; ++a) {
     std::string s = argv[a];
@@ -171,6 +175,7 @@ int main(int argc, char** argv) {
     }
     else if (s == "--window") window = strtoull(next(), nullptr, 10);
     else if (s == "--one-stream") one_stream = true;  // gpu: the walk on the stages' stream
+    else if (s == "--inline-results") inline_results = true;  // results walked on the main thread
     else die(("unknown option " + s).c_str(), -22);
   }
   batch = (batch + RTN_CHUNK_FRAMES - 1) / RTN_CHUNK_FRAMES * RTN_CHUNK_FRAMES;
@@ -255,10 +260,47 @@ int main(int argc, char** argv) {
   double t_wait = 0, t_walk = 0, t_pack = 0;  // host time split (seconds)
   auto now = [] { return std::chrono::steady_clock::now(); };
   auto secs_since = [&](std::chrono::steady_clock::time_point a) { return std::chrono::duration<double>(now() - a).count(); };
+  // A results thread walks the batches in capture order (waiting for each one's event), so the
+  // main thread only packs and enqueues; it waits for the thread before reusing a buffer set.
+  std::mutex mu;
+  std::condition_variable cv;
+  std::deque<uint32_t> queue;
+  bool stop = false;
+  double r_wait = 0, r_walk = 0;  // the results thread's time
+  std::thread results;
+  if (!inline_results)
+    results = std::thread([&] {
+      for (;;) {
+        uint32_t k;
+        {
+          std::unique_lock<std::mutex> l(mu);
+          cv.wait(l, [&] { return stop || !queue.empty(); });
+          if (queue.empty()) return;
+          k = queue.front();
+          queue.pop_front();
+        }
+        auto a = now();
+        HIP_CHECK(hipEventSynchronize(done[k]));
+        r_wait += secs_since(a);
+        a = now();
+        walk(hs[k], with_ct, t, dump);
+        r_walk += secs_since(a);
+        {
+          std::lock_guard<std::mutex> l(mu);
+          hs[k].pending = false;
+        }
+        cv.notify_all();
+      }
+    });
   const auto t0 = std::chrono::steady_clock::now();
   for (uint32_t it = 0;; ++it) {
     HostSet& h = hs[it & 1u];
-    if (h.pending) {  // results of batch it-2 (same buffers): wait, then walk them
+    if (!inline_results) {  // the results thread is done with batch it-2's buffers
+      auto a = now();
+      std::unique_lock<std::mutex> l(mu);
+      cv.wait(l, [&] { return !h.pending; });
+      t_wait += secs_since(a);
+    } else if (h.pending) {  // results of batch it-2 (same buffers): wait, then walk them
       auto a = now();
       HIP_CHECK(hipEventSynchronize(done[it & 1u]));
       t_wait += secs_since(a);
@@ -320,7 +362,25 @@ int main(int argc, char** argv) {
     HIP_CHECK(hipMemcpyAsync(h.addr6, out.addr6, rtn_out_addr6_bytes(n), hipMemcpyDeviceToHost, stream));
     if (with_ct) HIP_CHECK(hipMemcpyAsync(h.ct, d_ct, rtn_out_ct_bytes(n), hipMemcpyDeviceToHost, stream));
     HIP_CHECK(hipEventRecord(done[it & 1u], stream));
-    h.pending = true;
+    if (!inline_results) {
+      {
+        std::lock_guard<std::mutex> l(mu);
+        h.pending = true;
+        queue.push_back(it & 1u);
+      }
+      cv.notify_all();
+    } else {
+      h.pending = true;
+    }
+  }
+  if (!inline_results) {
+    {
+      std::lock_guard<std::mutex> l(mu);
+      stop = true;
+    }
+    cv.notify_all();
+    results.join();
+    t_walk = r_walk;
   }
   for (uint32_t k = 0; k < 2; ++k) {
     if (!hs[k].pending) continue;

@@ -64,11 +64,13 @@ def main() -> None:
         # fallback, worker threads copying them into pinned memory first (RTN_GPU_WALK_STAGED)
         # gpu-1s: the walk on the stages' stream (--one-stream)
         # gpu-w256m / gpu-w1g: 256-MiB / 1-GiB windows (default 64 MiB)
-        for name, layout in (("gpu", "gpu"), ("gpu-1s", "gpu"), ("gpu-staged", "gpu"), ("gpu-w256m", "gpu"),
-                             ("gpu-w1g", "gpu"), ("compact", "compact"), ("mono", "mono"), ("gpu", "gpu"),
-                             ("compact", "compact")):
+        # *-inline: the results walked on the main thread (--inline-results)
+        for name, layout in (("gpu", "gpu"), ("gpu-inline", "gpu"), ("gpu-1s", "gpu"), ("gpu-staged", "gpu"),
+                             ("gpu-w256m", "gpu"), ("gpu-w1g", "gpu"), ("compact", "compact"),
+                             ("compact-inline", "compact"), ("mono", "mono"), ("gpu", "gpu"), ("compact", "compact")):
             env = dict(os.environ, RTN_GPU_WALK_STAGED="1" if name == "gpu-staged" else "0")
-            more = {"gpu-1s": ["--one-stream"], "gpu-w256m": ["--window", str(256 << 20)],
+            more = {"gpu-inline": ["--inline-results"], "compact-inline": ["--inline-results"],
+                    "gpu-1s": ["--one-stream"], "gpu-w256m": ["--window", str(256 << 20)],
                     "gpu-w1g": ["--window", str(1 << 30)]}.get(name, [])
             for _ in range(2):  # the second run has the capture in the page cache
                 r = subprocess.run([str(exe), str(spec), str(cap), "--layout", layout, *extra, *more],
